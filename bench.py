@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: glacier energy-balance cell-updates/s on MI355X (BASELINE.json).
+
+One "step" = one model time step (BmiTopoflowGlacier.update(),
+bmi_topoflow_glacier.py:413-465) applied to every cell of the grid: read that
+hour's forcing frame from HBM, run the fused energy/mass balance, write the six
+BMI outputs of the step to HBM.  Steps are fused `--fuse` per kernel launch
+(state stays in registers between fused steps; every step still streams its
+forcing in and its outputs out).
+
+Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
+HBM-resident frames, fp32 engine (fp64 state).  --gpus N: one process per GPU
+(torchrun), row-block shards of 8192 rows each (weak scaling, no data-path
+collective); value = all cells of all ranks x steps / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.  Roofline: achieved = algorithmic bytes per
+fused launch / mean launch time (HIP events on the engine's stream).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT / "topoflow-glacier_amd"), str(ROOT)]
+
+METRIC = "cell-updates/sec (nx·ny·steps) on 8192² fp32 grid; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# algorithmic bytes per cell (DESIGN.md "Bytes per cell-update")
+BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs f32
+BYTES_PER_LAUNCH = 12 + (6 * 8 + 8) * 2  # static 3xf32; state 6xf64 + window total i64, in and out
+
+BASE_CFG = {
+    "site_prefix": "synthetic", "forcing_file": "synthetic", "dt": 1, "start_time": "2013032000",
+    "end_time": "2014032000", "da": 0.0001, "slope": 50.0, "aspect": 180.0, "lon": -121.81418,
+    "lat": 46.81953220, "elev": 2400.0, "h_active_layer": 0.125, "h0_snow": 5.0, "h0_ice": 2.0,
+    "h0_swe": 0.25, "h0_iwe": 1.834, "T_rain_snow": 0.0,
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=240)
+    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--ny", type=int, default=8192, help="rows per GPU (weak) or global rows (strong)")
+    ap.add_argument("--nx", type=int, default=8192)
+    ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--fuse", type=int, default=24)
+    ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--seed", type=int, default=20251001)
+    ap.add_argument("--cpu-cells", type=int, default=393216, help="cells in the CPU-baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=24)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, gpu_sample):
+    """Oracle (numpy fp64 restatement of the reference, 1 core) on the first
+    cells of rank 0's shard, same fp32 inputs; also a parity spot check."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import tfg_oracle as O
+
+    from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
+
+    n = min(args.cpu_cells, args.nx * args.ny)
+    steps = args.cpu_steps
+    syn = synthetic_cells(args.seed, np.arange(n), diurnal_table(args.frames))
+    frames = np.arange(steps) % args.frames
+    forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    static = dict(elev=syn["elev"], slope=syn["slope"], aspect=syn["aspect"], h0_snow=syn["h_snow"],
+                  h0_ice=syn["h_ice"], h0_swe=syn["h_swe"], h0_iwe=syn["h_iwe"])
+    static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
+    clock = O.oracle_clock(BASE_CFG["start_time"], BASE_CFG["dt"], steps, BASE_CFG["lon"])
+    t0 = time.perf_counter()
+    out, _ = O.run_oracle(BASE_CFG, static, forcing, steps, clock=(clock[0], clock[3]))
+    dt = time.perf_counter() - t0
+    parity = None
+    if gpu_sample is not None:
+        errs = []
+        for name, g in gpu_sample.items():
+            r = out[name][-1][: g.size]
+            s_v = np.percentile(np.abs(r), 99)
+            errs.append(float(np.max(np.abs(g - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300))))
+        parity = max(errs)
+    return {"value": n * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/tfg_oracle.py (numpy fp64 restatement of update(), single thread) on the first "
+                      f"{n} cells x {steps} hourly steps of the same synthetic workload ({dt:.1f} s)"}, parity
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+    from topoflow_glacier.sharding import allreduce_diagnostics, row_block
+    from topoflow_glacier.synthetic import diurnal_table
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.scaling == "weak":
+        ny_global = args.ny * world
+        row0, rows = rank * args.ny, args.ny
+    else:
+        ny_global = args.ny
+        row0, rows = row_block(args.ny, rank, world)
+    cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx))
+    eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0)
+    eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
+    stream = torch.cuda.Stream(local)  # a real (non-null) stream shared by the engine and the events
+    torch.cuda.set_stream(stream)
+    eng.set_stream(stream.cuda_stream)
+
+    def barrier():
+        torch.cuda.synchronize(local)
+        if world > 1:
+            dist.barrier()
+
+    # warmup (untimed)
+    eng.run(args.warmup)
+    barrier()
+    n_launch = max(1, args.steps // args.fuse)
+    steps = n_launch * args.fuse
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(n_launch):
+        ev[i][0].record(stream)
+        eng.run(args.fuse)
+        ev[i][1].record(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    cells = rows * args.nx
+    total_cells = ny_global * args.nx if args.scaling == "strong" else cells * world
+    value = total_cells * steps / elapsed
+    diag = allreduce_diagnostics(eng.diagnostics()) if world > 1 else eng.diagnostics()
+
+    gpu_sample = None
+    mean_launch_s = float(launch_ms.mean()) / 1e3
+    bytes_launch = cells * (BYTES_PER_STEP * args.fuse + BYTES_PER_LAUNCH)
+    achieved = bytes_launch / mean_launch_s / 1e9
+    eng.close()
+
+    result = None
+    if rank == 0:
+        cpu = None
+        parity = None
+        if not args.no_cpu_baseline:
+            # a short GPU run on the same sample cells for a parity spot check
+            n = min(args.cpu_cells, cells)
+            scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n))
+            se = GlacierEngine(scfg, 1, n, engine=args.engine, device=local, n_frames=args.frames,
+                               hist_depth=1, fuse_steps=args.fuse)
+            se.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=n)
+            se.run(args.cpu_steps)
+            se.sync()
+            gpu_sample = {k: se.get_field(k) for k in ("M_total", "SM", "IM", "RH", "h_snow")}
+            se.close()
+            cpu, parity = cpu_baseline(args, gpu_sample)
+        traffic = None
+        pmc = ROOT / "profiles" / f"pmc_{args.nx}x{args.ny}_fuse{args.fuse}.json"
+        if pmc.exists():
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        result = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "cell-updates/s",
+            "n_gpus": world,
+            "steps": steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / steps * 1e3,
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "f32" if args.engine == "float32" else "f64",
+            "data": "synthetic (counter-hash DEM/forcing with CSV statistics, 24 HBM-resident hourly frames)",
+            "config": {
+                "workload": f"{ny_global}x{args.nx} grid ({rows}x{args.nx} per GPU), hourly steps, "
+                            f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch",
+                "grid_per_gpu": [rows, args.nx],
+                "frames": args.frames,
+                "fuse_steps": args.fuse,
+                "parallelism": f"row-block x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
+                "kernel_ms_per_launch": float(launch_ms.mean()),
+            },
+            "cpu_baseline": cpu,
+            "sample_parity_floored_rel": parity,
+            "mass_balance": {k: float(v) for k, v in zip(["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"], diag[0])},
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

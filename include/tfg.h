@@ -1,0 +1,208 @@
+/*
+ * tfg.h -- C ABI of the MI355X glacier energy-balance engine (libtfg).
+ *
+ * The reference (NGWPC/topoflow-glacier v0.1.0) has no native code: its hot
+ * path is the pure-NumPy method BmiTopoflowGlacier.update()
+ * (src/topoflow_glacier/bmi/bmi_topoflow_glacier.py:413-465), one catchment
+ * per Python call.  This header is the boundary that replaces it: the Python
+ * BMI class (topoflow-glacier_amd/topoflow_glacier/bmi/bmi_topoflow_glacier.py)
+ * binds these entry points through ctypes (topoflow_glacier/_native.py).
+ * Each entry point names the reference interface it stands in for.
+ *
+ * Calling rules
+ *   - Every function returns an int status: 0 = TFG_OK, nonzero = error; the
+ *     message is then available from tfg_last_error(h) (or tfg_last_error(NULL)
+ *     for failures before a handle exists).  No C++ exception crosses the ABI.
+ *   - A handle owns all device buffers of one grid shard and one HIP stream.
+ *     Host pointers are borrowed for the duration of the call only.
+ *   - One thread per handle; calls on a handle are not re-entrant.
+ *   - Plain C types only: no torch / HIP types appear in the signatures
+ *     (streams are passed as void*).
+ */
+#ifndef TFG_H
+#define TFG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFG_ABI_VERSION 1
+
+/* status codes */
+enum {
+  TFG_OK = 0,
+  TFG_ERR_ARG = 1,     /* invalid argument (bad field id, size mismatch, null) */
+  TFG_ERR_HIP = 2,     /* a HIP runtime call failed                            */
+  TFG_ERR_STATE = 3,   /* call not valid in the handle's current state          */
+  TFG_ERR_DOMAIN = 4,  /* physically invalid input, e.g. slope angle out of
+                          [0, pi/2] (reference: set_slope_angle :1106-1111)    */
+};
+
+/* arithmetic of an engine / element type of a host or device buffer */
+enum {
+  TFG_F32 = 0, /* fp32 forcing/static/outputs, fp32 flux arithmetic, fp64 state */
+  TFG_F64 = 1, /* fp64 everywhere, reference operation order (bit-near parity)  */
+  TFG_I32 = 2, /* catchment-id raster only                                      */
+};
+
+/* Field ids.  Inputs follow _dynamic_input_vars (bmi_topoflow_glacier.py:18-26)
+ * and outputs _output_vars (:28-37) in the same order. */
+enum {
+  /* dynamic inputs (per forcing frame).  LW and SW are accepted for BMI
+   * completeness but the reference physics never reads them (:1122, :1235). */
+  TFG_IN_LW_IN = 0,  /* land_surface_radiation~incoming~longwave__energy_flux */
+  TFG_IN_P_AIR = 1,  /* land_surface_air__pressure [Pa]                         */
+  TFG_IN_HUM_SP = 2, /* atmosphere_air_water~vapor__relative_saturation (q)     */
+  TFG_IN_P = 3,      /* atmosphere_water__liquid_equivalent_precipitation_rate  */
+  TFG_IN_SW_IN = 4,  /* land_surface_radiation~incoming~shortwave__energy_flux  */
+  TFG_IN_T_AIR = 5,  /* land_surface_air__temperature [degC]                    */
+  TFG_IN_UZ = 6,     /* wind_speed_UV [m s-1]                                   */
+  /* BMI outputs (history slot addressable) */
+  TFG_OUT_H_SNOW = 7,  /* snowpack__depth                                       */
+  TFG_OUT_H_SWE = 8,   /* snowpack__liquid-equivalent_depth  (fp64 state)        */
+  TFG_OUT_SM = 9,      /* snowpack__melt_volume_flux                             */
+  TFG_OUT_H_ICE = 10,  /* glacier_ice__thickness                                 */
+  TFG_OUT_H_IWE = 11,  /* glacier__liquid_equivalent_depth    (fp64 state)        */
+  TFG_OUT_IM = 12,     /* glacier_ice__melt_volume_flux                          */
+  TFG_OUT_M_TOTAL = 13,/* land_surface_water__runoff_volume_flux                 */
+  TFG_OUT_RH = 14,     /* atmosphere_bottom_air_water-vapor__relative_saturation */
+  /* static rasters (config.py:19-28 scalars `elev`, `slope`, `aspect` become
+   * per-cell rasters) and the optional catchment-id raster */
+  TFG_ST_ELEV = 15,
+  TFG_ST_SLOPE = 16,
+  TFG_ST_ASPECT = 17,
+  TFG_ST_CATCH_ID = 18,
+  /* internal state (not BMI-visible in the reference, exposed for checkpoint) */
+  TFG_ST_ECCS = 19,   /* snowpack cold content  (:392, :1496-1564)           */
+  TFG_ST_ECCI = 20,   /* ice cold content       (:394, :1375-1434)           */
+  TFG_ST_ALBEDO = 21, /* albedo                 (:369, :1006-1059)           */
+  TFG_ST_NDAYS = 22,  /* days since major snowfall, as a step count (:1040)  */
+  TFG_NUM_FIELDS = 23
+};
+
+/* Diagnostics per catchment, in this order (:558-624, :1482-1494). */
+enum { TFG_DIAG_VOL_P = 0, TFG_DIAG_VOL_PR, TFG_DIAG_VOL_PS, TFG_DIAG_VOL_SM,
+       TFG_DIAG_VOL_IM, TFG_DIAG_P_MAX, TFG_NUM_DIAG };
+
+/* Model constants: TopoflowGlacierConfig (config.py:6-115) fields consumed by
+ * update(), plus the grid geometry the reference keeps as scalars. */
+typedef struct tfg_params {
+  double dt;             /* config.py:15 (hours; used as-is in energy terms)  */
+  double da_m2;          /* cell area [m2] (reference: da_km2*1e6, :293-294)   */
+  double lat, lon;       /* config.py:21-22 (uniform over the grid)           */
+  double sin_lat, cos_lat; /* sin/cos of lat*(pi/180), as the host computes them
+                              (Equivalent_Latitude SF:753-755)                  */
+  double T_rain_snow, dust_atten, canopy_factor, cloud_factor;
+  double rho_air, rho_snow, rho_ice, rho_H2O, h_active_layer, T0;
+  double Cp_air, Cp_ice, Cp_snow, g, Lf, eps, kappa, latent_heat_constant, Lv;
+  double sigma, sea_level_p0, uni_gas_const, M_mass_air, z0_air, em_surf;
+  int32_t satterlund;    /* config.py:101                                      */
+  int32_t ring_len;      /* int(3*24/dt) snowfall-window slots (:296)          */
+} tfg_params;
+
+/* Per-step uniform scalars, computed on the host in fp64 from the model clock
+ * (update_julian_day :957-1004 and the uniform part of Clear_Sky_Radiation,
+ * SF:894-953).  One record per time step. */
+typedef struct tfg_uniforms {
+  double th;         /* TSN_offset [h]                                (:1004) */
+  double omega_th;   /* omega*th [rad]                                  SF:867 */
+  double cos_wth;    /* cos(omega*th)                                           */
+  double sin_wth;    /* sin(omega*th)                                           */
+  double sin_d;      /* sin(declination)                                 SF:205 */
+  double cos_d;      /* cos(declination)                                        */
+  double tan_d;      /* tan(declination)                                 SF:325 */
+  double isc_e0;     /* Solar_Constant()*Eccentricity_Correction()       SF:869 */
+  double m_opt;      /* Optical_Air_Mass(lat, delta, th)                 SF:498 */
+  double k_et_flat;  /* ET_Radiation_Flux(lat, JD, th), clamped >= 0     SF:376 */
+  double flat_sr;    /* Sunrise_Offset(lat, delta)                       SF:305 */
+  double flat_ss;    /* Sunset_Offset(lat, delta)                        SF:334 */
+  /* fp32 copies of the fields above for the fp32 engine (host-rounded) */
+  float th_f, cos_wth_f, sin_wth_f, sin_d_f, cos_d_f, tan_d_f, isc_e0_f, m_opt_f;
+  float k_et_flat_f, flat_sr_f, flat_ss_f, pad_f;
+  int32_t frame;     /* forcing frame index this step reads                     */
+  int32_t hist;      /* output-history slot this step writes                    */
+  int32_t slot;      /* snowfall-window ring slot (step mod ring_len)           */
+  int32_t pad;
+} tfg_uniforms;
+
+typedef struct tfg_handle tfg_handle;
+
+/* Library / device info. */
+int tfg_abi_version(void);
+const char* tfg_build_info(void);
+int tfg_device_count(int* count);
+
+/* Create one grid shard of ny*nx cells on `device`.
+ *   engine      TFG_F32 or TFG_F64
+ *   n_frames    forcing frames resident on the device (>= 1)
+ *   hist_depth  output-history slots (>= 1); step k writes slot u[k].hist
+ *   n_catch     catchments for the mass-balance diagnostics (>= 1)
+ * Replaces: BmiTopoflowGlacier.__init__ + initialize() array setup
+ * (bmi_topoflow_glacier.py:118-122, :281-395). */
+int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int device,
+               int n_frames, int hist_depth, int n_catch, tfg_handle** out);
+
+/* Release everything.  Replaces: finalize() (:467-469). */
+int tfg_destroy(tfg_handle* h);
+
+/* Run the work on a caller-provided HIP stream (hipStream_t as void*), or
+ * NULL to return to the handle's own stream. */
+int tfg_set_stream(tfg_handle* h, void* stream);
+int tfg_get_stream(tfg_handle* h, void** stream);
+
+/* Copy n cells into a field.  `index` is the forcing frame for TFG_IN_*,
+ * ignored otherwise.  src_dtype is the element type of `src`; it is converted
+ * on the device.  src_on_device != 0 means `src` is a device pointer.
+ * Replaces: set_value / Context.set_value (:1800-1802, context.py:42-44). */
+int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_dtype,
+                  int64_t n, int src_on_device);
+
+/* Copy n cells of a field out.  `index` is the history slot for TFG_OUT_*
+ * (except H_SWE/H_IWE, which are state), the frame for TFG_IN_*.
+ * Replaces: get_value / get_value_ptr (:1810-1828). */
+int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n,
+                  int dst_on_device);
+
+/* (Re)initialise the internal state from the current depth fields: cold
+ * contents Eccs/Ecci (:389-395), albedo 0.3 (:369), days-since-snowfall 0
+ * (:288), empty snowfall window (:296), zero diagnostics (:314-317, :362-363).
+ * Call after the initial h_snow/h_ice/h_swe/h_iwe rasters are set. */
+int tfg_init_state(tfg_handle* h);
+
+/* Advance nsteps time steps; u[k] are the uniforms of step k.
+ * Replaces: update() (:413-465) when nsteps == 1 and update_until()
+ * (:471-490) otherwise.  Steps are fused into multi-step launches that keep
+ * the per-cell state in registers; every step still reads its forcing frame
+ * and writes its six outputs to history slot u[k].hist. */
+int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps);
+
+/* Maximum steps fused into one launch (default 24; 1 disables fusion). */
+int tfg_set_fuse(tfg_handle* h, int max_steps_per_launch);
+
+/* Mass-balance diagnostics, out[n_catch][TFG_NUM_DIAG] (fp64, blocking).
+ * Replaces: the vol_P/vol_PR/vol_PS/vol_SM/vol_IM integrals and P_max
+ * (:558-624, :1482-1494). */
+int tfg_get_diag(tfg_handle* h, double* out, int n_catch);
+int tfg_reset_diag(tfg_handle* h);
+
+/* Wait for all work queued on the handle's stream. */
+int tfg_sync(tfg_handle* h);
+
+/* Device-side synthetic workload generator (bench / tests): fills the forcing
+ * frames, static rasters and initial depths from a counter-based hash of
+ * (seed, field, frame, global cell index).  `row0` is this shard's first row in
+ * the global grid so shards of one grid agree with an unsharded run.
+ * `diurnal` holds n_frames fp32 diurnal-cycle factors.  The host mirror is
+ * topoflow_glacier/synthetic.py (bit-identical fp32 values). */
+int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_global,
+                       const float* diurnal, int n_frames);
+
+/* Last error message of a handle (NULL: the last create/global error). */
+const char* tfg_last_error(const tfg_handle* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFG_H */

@@ -1,0 +1,186 @@
+"""Shared test machinery: golden-fixture loading, the oracle runner, and the
+GPU-vs-oracle comparison with the parity tolerance of SURVEY.md 8(d).
+
+Test infrastructure only (imports the oracle as the checker).
+"""
+
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+from types import SimpleNamespace
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+for p in (str(ROOT / "topoflow-glacier_amd"), str(ROOT / "oracle"), str(ROOT)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import tfg_oracle as O  # noqa: E402
+
+OUT_NAMES = ["h_snow", "h_swe", "SM", "h_ice", "h_iwe", "IM", "M_total", "RH"]
+STATIC_KEYS = ["elev", "slope", "aspect", "h0_snow", "h0_ice", "h0_swe", "h0_iwe"]
+
+# cat-3062920 (tests/integration_test.py:20-38 of the reference)
+BASE_CFG = {
+    "site_prefix": "cat-3062920", "forcing_file": "data/sample-cat-3062920.csv", "dt": 1,
+    "start_time": "2013032000", "end_time": "2013033100", "da": 11.418749923500716,
+    "slope": 88.582729, "aspect": 242.8644693769529, "lon": -121.81418, "lat": 46.81953220,
+    "elev": 2446.3922737596167, "h_active_layer": 0.125, "h0_snow": 5.0, "h0_ice": 2.0,
+    "h0_swe": 0.25, "h0_iwe": 1.834, "T_rain_snow": 0.0,
+}
+
+
+def load_golden(name: str) -> dict:
+    z = np.load(GOLDEN / f"{name}.npz")
+    cells = json.loads(str(z["cell_cfgs"]))
+    F = z["forcing"]
+    return {
+        "cfg": dict(cells[0]),
+        "cells": cells,
+        "static": {k: np.array([c[k] for c in cells], dtype=np.float64) for k in STATIC_KEYS},
+        "forcing": {n: F[i] for i, n in enumerate(z["in_names"])},  # [nsteps][ncell]
+        "outputs": {n: z["outputs"][j] for j, n in enumerate(z["out_names"])},
+        "internal": {n: z["internal"][j] for j, n in enumerate(z["internal_names"])},
+        "nsteps": F.shape[1],
+        "ncell": F.shape[2],
+    }
+
+
+def cfg_object(cfg: dict):
+    """A TopoflowGlacierConfig from a plain dict (product loader)."""
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+
+    return TopoflowGlacierConfig.model_validate(cfg)
+
+
+def oracle_run(cfg: dict, static: dict, forcing: dict, nsteps: int | None = None, catch_id=None):
+    out, m = O.run_oracle(cfg, {"elev": static["elev"], "slope": static["slope"], "aspect": static["aspect"],
+                                "h0_snow": static["h0_snow"], "h0_ice": static["h0_ice"],
+                                "h0_swe": static["h0_swe"], "h0_iwe": static["h0_iwe"]}, forcing, nsteps)
+    return out, m
+
+
+def parity(gpu: np.ndarray, ref: np.ndarray, rtol: float = 1e-5):
+    """Floored relative error |gpu-ref| / max(|ref|, s_v), s_v = p99 |ref|.
+
+    Returns (max floored error, fraction of elements above pure-relative rtol).
+    """
+    gpu = np.asarray(gpu, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    s_v = float(np.percentile(np.abs(ref), 99)) if ref.size else 0.0
+    floor = np.maximum(np.abs(ref), s_v)
+    err = np.abs(gpu - ref)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        fl = np.where(floor > 0, err / floor, np.where(err > 0, np.inf, 0.0))
+        rel = np.where(np.abs(ref) > 0, err / np.abs(ref), np.where(err > 0, np.inf, 0.0))
+    return float(np.max(fl)) if fl.size else 0.0, float(np.mean(rel > rtol)) if rel.size else 0.0
+
+
+def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
+                fuse_steps: int = 24):
+    from topoflow_glacier.engine import GlacierEngine
+
+    return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
+                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps)
+
+
+def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,
+                   fuse_steps: int = 24, catch_id=None, n_catch: int = 1, chunks=None):
+    """Run the GPU engine on explicit per-step forcing (one frame per step).
+
+    Returns (dict name -> [nsteps][ncell] outputs, state dict, diagnostics)."""
+    n = ny * nx
+    eng = make_engine(cfg, ny, nx, engine, n_frames=nsteps, hist_depth=nsteps, n_catch=n_catch, fuse_steps=fuse_steps)
+    try:
+        for k in ("elev", "slope", "aspect"):
+            eng.set_field(k, static[k])
+        for k in ("h_snow", "h_ice", "h_swe", "h_iwe"):
+            eng.set_field(k, static["h0_" + k[2:]])
+        if catch_id is not None:
+            eng.set_field("catch_id", catch_id)
+        eng.init_state()
+        for k in range(nsteps):
+            for name in ("P", "T_air", "Hum_sp", "P_air", "uz"):
+                eng.set_field(name, np.asarray(forcing[name][k]).reshape(n), index=k)
+        frames = np.arange(nsteps, dtype=np.int32)
+        if chunks is None:
+            eng.run(nsteps, frames=frames)
+        else:
+            done = 0
+            for c in chunks:
+                eng.run(c, frames=frames[done:done + c])
+                done += c
+        eng.sync()
+        outs = {name: np.stack([eng.get_field(name, index=k) for k in range(nsteps)])
+                for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")}
+        state = {name: eng.get_field(name) for name in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")}
+        diag = eng.diagnostics()
+        return outs, state, diag
+    finally:
+        eng.close()
+
+
+def synthetic_inputs(seed: int, ny: int, nx: int, n_frames: int, row0: int = 0):
+    from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
+
+    d = diurnal_table(n_frames)
+    cells = (np.arange(ny)[:, None] + row0) * nx + np.arange(nx)[None, :]
+    return synthetic_cells(seed, cells.reshape(-1), d), d
+
+
+def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", seed: int = 7,
+                      n_frames: int = 24, fuse_steps: int = 24, cfg_over: dict | None = None):
+    """Device-generated synthetic workload on the GPU vs the oracle on the same
+    fp32 inputs (host mirror).  Returns a report dict."""
+    cfg = dict(BASE_CFG)
+    cfg.update(cfg_over or {})
+    syn, diurnal = synthetic_inputs(seed, ny, nx, n_frames)
+    eng = make_engine(cfg, ny, nx, engine, n_frames=n_frames, hist_depth=nsteps, fuse_steps=fuse_steps)
+    try:
+        eng.fill_synthetic(seed, diurnal)
+        eng.run(nsteps)
+        eng.sync()
+        gpu = {name: np.stack([eng.get_field(name, index=k) for k in range(nsteps)])
+               for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")}
+        gpu["h_swe"] = eng.get_field("h_swe")
+        gpu["h_iwe"] = eng.get_field("h_iwe")
+        diag = eng.diagnostics()
+    finally:
+        eng.close()
+    frames = np.arange(nsteps) % n_frames
+    forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"],
+              "h0_snow": syn["h_snow"], "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
+    static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
+    ref, m = oracle_run(cfg, static, forcing, nsteps)
+    report = {}
+    worst = 0.0
+    worst_rel = 0.0
+    for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH"):
+        e, frac = parity(gpu[name], ref[name])
+        report[name] = (e, frac)
+        worst = max(worst, e)
+    for name in ("h_swe", "h_iwe"):
+        e, frac = parity(gpu[name], ref[name][-1])
+        report[name] = (e, frac)
+        worst = max(worst, e)
+    dref = np.array([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max])
+    dg = diag.sum(axis=0)
+    dg[5] = diag[:, 5].max()
+    with np.errstate(divide="ignore", invalid="ignore"):
+        drel = np.where(dref != 0, np.abs(dg - dref) / np.abs(dref), np.abs(dg - dref))
+    report["diag"] = (float(np.max(drel)), 0.0)
+    worst_rel = max(worst, float(np.max(drel)))
+    tol = 1e-5 if engine == "float32" else 1e-9
+    ok = worst_rel <= tol
+    summary = ", ".join(f"{k}={v[0]:.2e}" for k, v in report.items())
+    return {"ok": ok, "max_rel": worst_rel, "report": report, "summary": summary, "gpu": gpu, "ref": ref,
+            "diag": dg, "diag_ref": dref}
+
+
+def ns(**kw):
+    return SimpleNamespace(**kw)

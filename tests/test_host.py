@@ -1,0 +1,190 @@
+"""Host-side product logic on CPU: clock/uniforms, config loader, C-ABI library
+(loads, exports every header symbol, struct layouts), synthetic generator."""
+
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import yaml
+
+from tests.harness import BASE_CFG, GOLDEN, ROOT, load_golden
+
+import tfg_oracle as O  # noqa: E402  (checker)
+
+
+# ----------------------------------------------------------------- clock
+@pytest.mark.parametrize("name", ["cat3062920_265", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter"])
+def test_clock_matches_reference(name):
+    from topoflow_glacier.physics.clock import StepClock
+
+    g = load_golden(name)
+    c = g["cfg"]
+    clk = StepClock(c["start_time"], c["dt"], c["lat"], c["lon"])
+    jd, yr, gmt, tsn = clk.calendar(0, g["nsteps"])
+    assert np.array_equal(jd, g["internal"]["julian_day"][:, 0])
+    assert np.array_equal(gmt, g["internal"]["GMT_offset"][:, 0])
+    assert np.array_equal(tsn, g["internal"]["TSN_offset"][:, 0])  # bit-exact
+
+
+def test_uniforms_match_oracle_functions():
+    from topoflow_glacier.physics.clock import StepClock
+
+    c = BASE_CFG
+    clk = StepClock(c["start_time"], c["dt"], c["lat"], c["lon"])
+    u = clk.uniforms(5, 200)
+    jd, _, _, tsn = O.oracle_clock(c["start_time"], c["dt"], 205, c["lon"])
+    jd, tsn = jd[5:], tsn[5:]
+    delta = O.declination(O.day_angle(jd))
+    assert np.array_equal(u["th"], tsn)
+    assert np.array_equal(u["sin_d"], np.sin(delta)) and np.array_equal(u["tan_d"], np.tan(delta))
+    assert np.array_equal(u["isc_e0"], np.float64(1361.5) * O.eccentricity_correction(O.day_angle(jd)))
+    assert np.array_equal(u["m_opt"], O.optical_air_mass(c["lat"], delta, tsn))
+    assert np.array_equal(u["k_et_flat"], O.et_radiation_flux(c["lat"], jd, tsn))
+    assert np.array_equal(u["flat_sr"], O.sunrise_offset(c["lat"], delta))
+    assert np.array_equal(u["flat_ss"], O.sunset_offset(c["lat"], delta))
+    assert np.array_equal(u["omega_th"], O.earth_angular_velocity() * tsn)
+    assert np.array_equal(u["slot"], np.arange(5, 205) % 72)
+    assert np.array_equal(u["th_f"], tsn.astype(np.float32))
+
+
+def test_time_zone_lookup_and_errors():
+    from topoflow_glacier.physics.clock import StepClock, zone_for
+
+    assert zone_for(46.8, -121.8) == "America/Los_Angeles"
+    assert zone_for(60.4, -148.9) == "America/Anchorage"  # Wolverine glacier
+    with pytest.raises(ValueError):
+        zone_for(0.0, 0.0)
+    with pytest.raises(ValueError):
+        StepClock("2070010100", 1, 46.8, -121.8).calendar(0, 2)  # perihelion table 1981-2060
+
+
+# ----------------------------------------------------------------- config
+REF_CONFIGS = sorted((ROOT / "tests" / "golden" / "config").glob("*.yaml"))
+
+
+def test_reference_yamls_validate():
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+
+    assert REF_CONFIGS, "reference config fixtures missing"
+    for p in REF_CONFIGS:
+        cfg = TopoflowGlacierConfig.model_validate(yaml.safe_load(p.read_text()))
+        assert isinstance(cfg.dt, int) and cfg.dt == 1
+        assert (cfg.ny, cfg.nx) == (1, 1)
+
+
+def test_config_defaults_match_oracle_and_extensions():
+    from pydantic import ValidationError
+
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+
+    cfg = TopoflowGlacierConfig.model_validate(BASE_CFG)
+    for k, v in O.CFG_DEFAULTS.items():
+        if k in BASE_CFG:
+            continue
+        assert getattr(cfg, k) == v, k
+    q = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, dt=0.25, ny=128, nx=64, engine="float32"))
+    assert q.dt == 0.25 and q.ny == 128 and q.engine == "float32"
+    with pytest.raises(ValidationError):
+        TopoflowGlacierConfig.model_validate(dict(BASE_CFG, dust_atten=0.5))
+    with pytest.raises(ValidationError):
+        TopoflowGlacierConfig.model_validate({k: v for k, v in BASE_CFG.items() if k != "lat"})
+
+
+def test_params_from_config():
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import params_from_config
+
+    p = params_from_config(TopoflowGlacierConfig.model_validate(dict(BASE_CFG, dt=0.25)))
+    assert p.ring_len == 288 and p.dt == 0.25
+    assert p.da_m2 == BASE_CFG["da"] * 1e6
+    lat_rad = BASE_CFG["lat"] * (np.pi / np.float64(180))
+    assert p.sin_lat == np.sin(lat_rad) and p.cos_lat == np.cos(lat_rad)
+
+
+# ----------------------------------------------------------------- C ABI
+def _header_functions():
+    txt = (ROOT / "include" / "tfg.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(tfg_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from topoflow_glacier import _native
+
+    L = _native.load()
+    names = _header_functions()
+    assert len(names) >= 17
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing
+    assert L.tfg_abi_version() == 1
+    assert b"gfx950" in L.tfg_build_info()
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """Compile a probe against include/tfg.h with gcc and compare sizes/offsets
+    with the ctypes / numpy mirrors."""
+    from topoflow_glacier import _native
+
+    src = tmp_path / "probe.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stddef.h>\n#include "tfg.h"\n'
+        "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(tfg_params), offsetof(tfg_params, satterlund),"
+        " sizeof(tfg_uniforms), offsetof(tfg_uniforms, th_f), offsetof(tfg_uniforms, frame), offsetof(tfg_uniforms, slot));return 0;}\n"
+    )
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    U = _native.UNIFORM_DTYPE
+    assert got == [ctypes.sizeof(_native.TfgParams), _native.TfgParams.satterlund.offset,
+                   U.itemsize, U.fields["th_f"][1], U.fields["frame"][1], U.fields["slot"][1]]
+
+
+def test_no_gpu_fails_loudly():
+    """Without a HIP device the engine raises; there is no CPU fallback."""
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from topoflow_glacier import _native
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+
+    with pytest.raises(_native.NativeError):
+        GlacierEngine(TopoflowGlacierConfig.model_validate(BASE_CFG), 4, 4, engine="float32", device=0)
+
+
+def test_bmi_surface_without_gpu():
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    m = BmiTopoflowGlacier()
+    assert m.get_component_name() == "Topoflow-Glacier"
+    assert len(m.get_input_var_names()) == 7 and len(m.get_output_var_names()) == 8
+    assert m.get_input_var_names()[5] == "land_surface_air__temperature"
+    assert m.get_var_units("snowpack__depth") == "m"
+    assert m.get_var_itemsize("snowpack__depth") == 8 and m.get_var_nbytes("snowpack__depth") == 8
+    assert "float" in m.get_var_type("snowpack__depth")
+    with pytest.raises(KeyError):
+        m.get_value_ptr("no_such_variable")
+    m.set_value("land_surface_air__temperature", np.array([273.15]))
+    assert m.get_value("land_surface_air__temperature", np.zeros(1))[0] == 273.15
+
+
+# ----------------------------------------------------------------- synthetic
+def test_synthetic_mirror_is_deterministic_and_in_range():
+    from topoflow_glacier.synthetic import diurnal_table, hash_u01, synthetic_cells
+
+    d = diurnal_table(24)
+    a = synthetic_cells(7, np.arange(1000), d)
+    b = synthetic_cells(7, np.arange(500, 1000), d)
+    for k in a:
+        assert a[k].dtype == np.float32
+        assert np.array_equal(a[k][..., 500:], b[k]), k  # cell-addressable
+    assert a["T_air"].shape == (24, 1000)
+    assert 1500 <= a["elev"].min() and a["elev"].max() <= 3000
+    assert (a["slope"] >= 0.5).all() and (a["P"] >= 0).all()
+    frac = (a["P"] > 0).mean()
+    assert 0.2 < frac < 0.28
+    u = hash_u01(1, 0, 0, np.arange(100000))
+    assert 0.0 <= u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01

@@ -1,0 +1,994 @@
+// tfg_engine.hip -- MI355X (gfx950) glacier energy-balance engine: kernels and
+// the C ABI declared in include/tfg.h.
+//
+// Hot path: k_fused<R, EXACT, READ_DEPTHS, CATCH> advances every cell of the
+// shard by K consecutive time steps in ONE launch.  A thread owns C adjacent
+// cells (C*sizeof(R) = 16 B: one dwordx4 per field per wave-lane); it loads the
+// cells' static rasters and fp64 state once, keeps the state in registers for
+// the K steps, and per step streams in the step's forcing frame and the
+// expiring snowfall-window slot and streams out the new slot and the six BMI
+// outputs.  There is no lateral coupling in the reference physics (Qc = Qa = 0,
+// bmi_topoflow_glacier.py:936-955), so no LDS tile or halo is needed; LDS only
+// holds the per-wave mass-balance bins.
+//
+// Mass-balance diagnostics (vol_P/PR/PS/SM/IM, P_max: :558-624, :1482-1494)
+// are reduced without atomics: lane registers -> wave butterfly (__shfl_xor) ->
+// per-wave LDS bins -> one slab row per workgroup -> k_diag_reduce, which folds
+// the slab into the running fp64 totals in a fixed order (bitwise
+// reproducible).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/tfg.h"
+#include "tfg_physics.hpp"
+
+namespace {
+
+using tfg::CellDiag;
+using tfg::CellOut;
+using tfg::CellState;
+using tfg::CellStatic;
+using tfg::CellStaticF;
+using tfg::DevParams;
+
+constexpr int kBlock = 256;
+#ifndef TFG_CELLS_PER_THREAD
+#define TFG_CELLS_PER_THREAD 1
+#endif
+constexpr int kCellsPerThread = TFG_CELLS_PER_THREAD;  // adjacent cells per lane
+constexpr int kWaves = kBlock / 64;
+constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
+constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
+constexpr int kNumHist = 6;   // h_snow, SM, h_ice, IM, M_total, RH
+enum { S_HSWE = 0, S_HIWE, S_ECCS, S_ECCI, S_N, S_ALB, S_HSNOW, S_HICE };
+enum { F_P = 0, F_T, F_Q, F_PA, F_UZ };
+enum { H_HSNOW = 0, H_SM, H_HICE, H_IM, H_MTOT, H_RH };
+
+struct KArgs {
+  DevParams p;
+  const void* forc;       // [n_frames][5][n_pad] R
+  const void* stat;       // [3][n_pad] R: elev, slope, aspect
+  const int32_t* catch_id;  // [n_pad] or nullptr
+  double* st;             // [8][n_pad]
+  int64_t* tot;           // [n_pad]
+  int32_t* ring;          // [ring_len][n_pad]
+  void* hist;             // [hist_depth][6][n_pad] R
+  double* slab;           // [gridDim][n_catch][6]
+  const tfg_uniforms* u;  // [K]
+  int K;
+  int n_catch;
+  int64_t n, n_pad;
+};
+
+// Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
+template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
+
+template <class T, int C>
+__device__ __forceinline__ void vload(const T* __restrict__ p, T (&v)[C]) {
+  const Pack<T, C> x = *reinterpret_cast<const Pack<T, C>*>(p);
+#pragma unroll
+  for (int j = 0; j < C; ++j) v[j] = x.v[j];
+}
+template <class T, int C>
+__device__ __forceinline__ void vstore(T* __restrict__ p, const T (&v)[C]) {
+  Pack<T, C> x;
+#pragma unroll
+  for (int j = 0; j < C; ++j) x.v[j] = v[j];
+  *reinterpret_cast<Pack<T, C>*>(p) = x;
+}
+template <int C> __device__ __forceinline__ void dload(const double* p, double (&v)[C]) { vload<double, C>(p, v); }
+template <int C> __device__ __forceinline__ void dstore(double* p, const double (&v)[C]) { vstore<double, C>(p, v); }
+template <int C> __device__ __forceinline__ void iload(const int32_t* p, int32_t (&v)[C]) { vload<int32_t, C>(p, v); }
+template <int C> __device__ __forceinline__ void istore(int32_t* p, const int32_t (&v)[C]) { vstore<int32_t, C>(p, v); }
+template <int C> __device__ __forceinline__ void lload(const int64_t* p, int64_t (&v)[C]) { vload<int64_t, C>(p, v); }
+template <int C> __device__ __forceinline__ void lstore(int64_t* p, const int64_t (&v)[C]) { vstore<int64_t, C>(p, v); }
+
+__device__ __forceinline__ void diag_zero(CellDiag& d) {
+  d.P = d.PR = d.PS = d.SM = d.IM = 0.0;
+  d.Pmax = -INFINITY;
+}
+
+// Fold the lanes' partial sums into this wave's LDS bins, one pass per
+// distinct catchment id present in the wave (normally one).  All 64 lanes
+// must be active.  Fixed butterfly order -> deterministic.
+__device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, const CellDiag& d, bool has) {
+  const int lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(has);
+  while (pending) {
+    const int leader = __builtin_ctzll(pending);
+    const int c = __shfl(cid, leader);
+    const bool mine = has && (cid == c);
+    double v0 = mine ? d.P : 0.0, v1 = mine ? d.PR : 0.0, v2 = mine ? d.PS : 0.0;
+    double v3 = mine ? d.SM : 0.0, v4 = mine ? d.IM : 0.0, m = mine ? d.Pmax : -INFINITY;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      v0 += __shfl_xor(v0, off);
+      v1 += __shfl_xor(v1, off);
+      v2 += __shfl_xor(v2, off);
+      v3 += __shfl_xor(v3, off);
+      v4 += __shfl_xor(v4, off);
+      m = tfg::npmax(m, __shfl_xor(m, off));
+    }
+    if (lane == leader) {
+      double* b = wbins + 6 * c;
+      b[0] += v0; b[1] += v1; b[2] += v2; b[3] += v3; b[4] += v4;
+      b[5] = tfg::npmax(b[5], m);
+    }
+    pending &= ~__ballot(mine);
+  }
+}
+
+template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
+__global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
+  extern __shared__ double lds_bins[];  // [kWaves][n_catch][6]
+  const DevParams& p = a.p;
+  const int nb = a.n_catch * 6;
+  for (int i = threadIdx.x; i < kWaves * nb; i += kBlock) lds_bins[i] = ((i % 6) == 5) ? -INFINITY : 0.0;
+  __syncthreads();
+  double* wbins = lds_bins + (threadIdx.x >> 6) * nb;
+
+  const int64_t n_pad = a.n_pad;
+  const int64_t ngroups = n_pad / C;
+  const int64_t g0 = (int64_t)blockIdx.x * ngroups / gridDim.x;
+  const int64_t g1 = ((int64_t)blockIdx.x + 1) * ngroups / gridDim.x;
+  const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
+  const R* __restrict__ forc = static_cast<const R*>(a.forc);
+  const R* __restrict__ stat = static_cast<const R*>(a.stat);
+  R* __restrict__ hist = static_cast<R*>(a.hist);
+  double* __restrict__ st = a.st;
+  using StaticT = typename std::conditional<EXACT, CellStatic, CellStaticF>::type;
+
+  CellDiag acc;
+  diag_zero(acc);
+
+  for (int64_t it = 0; it < trips; ++it) {
+    const int64_t g = g0 + it * kBlock + threadIdx.x;
+    const bool in = g < g1;
+    int32_t cid[C];
+    CellDiag cacc[CATCH ? C : 1];
+    if constexpr (CATCH) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) { diag_zero(cacc[j]); cid[j] = 0; }
+    }
+    if (in) {
+      const int64_t c0 = g * C;
+      if constexpr (CATCH) iload<C>(a.catch_id + c0, cid);
+      // static rasters -> per-cell solar geometry (fp64 derivation), once per launch
+      StaticT S[C];
+      {
+        R el[C], sl[C], as[C];
+        vload<R, C>(stat + c0, el);
+        vload<R, C>(stat + n_pad + c0, sl);
+        vload<R, C>(stat + 2 * n_pad + c0, as);
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          if constexpr (EXACT) S[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
+          else S[j] = tfg::derive_static_f(p, (double)el[j], (double)sl[j], (double)as[j]);
+        }
+      }
+      // state
+      CellState cs[C];
+      {
+        double v[C];
+        dload<C>(st + S_HSWE * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].h_swe = v[j];
+        dload<C>(st + S_HIWE * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].h_iwe = v[j];
+        dload<C>(st + S_ECCS * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].Eccs = v[j];
+        dload<C>(st + S_ECCI * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].Ecci = v[j];
+        dload<C>(st + S_N * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].n = v[j];
+        dload<C>(st + S_ALB * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].albedo = v[j];
+        if constexpr (READ_DEPTHS) {
+          dload<C>(st + S_HSNOW * n_pad + c0, v);
+#pragma unroll
+          for (int j = 0; j < C; ++j) cs[j].h_snow = v[j];
+          dload<C>(st + S_HICE * n_pad + c0, v);
+#pragma unroll
+          for (int j = 0; j < C; ++j) cs[j].h_ice = v[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            cs[j].h_snow = cs[j].h_swe * p.ws;  // :1711, bit-identical to the last step
+            cs[j].h_ice = cs[j].h_iwe * p.wi;   // :1726
+          }
+        }
+        int64_t t[C];
+        lload<C>(a.tot + c0, t);
+#pragma unroll
+        for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
+      }
+
+      for (int k = 0; k < a.K; ++k) {
+        const tfg_uniforms* up = a.u + k;
+        const tfg_uniforms u = *up;
+        const R* __restrict__ fr = forc + (int64_t)u.frame * kNumForc * n_pad + c0;
+        R P[C], T[C], Q[C], PA[C], UZ[C];
+        vload<R, C>(fr + F_P * n_pad, P);
+        vload<R, C>(fr + F_T * n_pad, T);
+        vload<R, C>(fr + F_Q * n_pad, Q);
+        vload<R, C>(fr + F_PA * n_pad, PA);
+        vload<R, C>(fr + F_UZ * n_pad, UZ);
+        int32_t* __restrict__ slot = a.ring + (int64_t)u.slot * n_pad + c0;
+        int32_t qo[C], qn[C];
+        iload<C>(slot, qo);
+        R o_hs[C], o_sm[C], o_hi[C], o_im[C], o_mt[C], o_rh[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          CellOut o;
+          CellDiag& d = CATCH ? cacc[j] : acc;
+          const bool valid = (c0 + j) < a.n;
+          if constexpr (EXACT) {
+            tfg::cell_step_exact(p, S[j], u, (double)P[j], (double)T[j], (double)Q[j], (double)PA[j],
+                                 (double)UZ[j], qo[j], qn[j], cs[j], o, d, valid);
+          } else {
+            tfg::cell_step_fast(p, S[j], up, u, (float)P[j], (float)T[j],
+                                (float)Q[j], (float)PA[j], (float)UZ[j], qo[j], qn[j], cs[j], o, d, valid);
+          }
+          o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
+          o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
+        }
+        istore<C>(slot, qn);
+        R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad + c0;
+        vstore<R, C>(h + H_HSNOW * n_pad, o_hs);
+        vstore<R, C>(h + H_SM * n_pad, o_sm);
+        vstore<R, C>(h + H_HICE * n_pad, o_hi);
+        vstore<R, C>(h + H_IM * n_pad, o_im);
+        vstore<R, C>(h + H_MTOT * n_pad, o_mt);
+        vstore<R, C>(h + H_RH * n_pad, o_rh);
+      }
+      // write back state
+      {
+        double v[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].h_swe;
+        dstore<C>(st + S_HSWE * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].h_iwe;
+        dstore<C>(st + S_HIWE * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].Eccs;
+        dstore<C>(st + S_ECCS * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].Ecci;
+        dstore<C>(st + S_ECCI * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].n;
+        dstore<C>(st + S_N * n_pad + c0, v);
+#pragma unroll
+        for (int j = 0; j < C; ++j) v[j] = cs[j].albedo;
+        dstore<C>(st + S_ALB * n_pad + c0, v);
+        int64_t t[C];
+#pragma unroll
+        for (int j = 0; j < C; ++j) t[j] = cs[j].tot_q;
+        lstore<C>(a.tot + c0, t);
+      }
+    }
+    if constexpr (CATCH) {
+#pragma unroll
+      for (int j = 0; j < C; ++j) wave_flush(wbins, cid[j], cacc[j], in);
+    }
+  }
+  if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
+  __syncthreads();
+  double* slab = a.slab + (int64_t)blockIdx.x * nb;
+  for (int i = threadIdx.x; i < nb; i += kBlock) {
+    double v = lds_bins[i];
+    if ((i % 6) == 5) {
+      for (int w = 1; w < kWaves; ++w) v = tfg::npmax(v, lds_bins[w * nb + i]);
+    } else {
+      for (int w = 1; w < kWaves; ++w) v += lds_bins[w * nb + i];
+    }
+    slab[i] = v;
+  }
+}
+
+// acc[i] (+)= reduce over blocks of slab[b][i]; one workgroup per diag entry.
+__global__ __launch_bounds__(kBlock) void k_diag_reduce(const double* __restrict__ slab, int nblocks, int nb,
+                                                        double* __restrict__ acc) {
+  __shared__ double red[kBlock];
+  const int i = blockIdx.x;
+  const bool is_max = (i % 6) == 5;
+  double v = is_max ? -INFINITY : 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) {
+    const double x = slab[(int64_t)b * nb + i];
+    v = is_max ? tfg::npmax(v, x) : v + x;
+  }
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = kBlock / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const double o = red[threadIdx.x + s];
+      red[threadIdx.x] = is_max ? tfg::npmax(red[threadIdx.x], o) : red[threadIdx.x] + o;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) acc[i] = is_max ? tfg::npmax(acc[i], red[0]) : acc[i] + red[0];
+}
+
+template <class D, class S>
+__global__ void k_convert(D* __restrict__ dst, const S* __restrict__ src, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (D)src[i];
+}
+
+// initialize() state (:389-395, :369, :288, :296) from the current depths
+__global__ void k_init_state(double* __restrict__ st, int64_t n_pad, double rhoCp_snow, double del_T,
+                             double Ecci0) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
+    const double e = rhoCp_snow * st[S_HSNOW * n_pad + i] * del_T;
+    st[S_ECCS * n_pad + i] = tfg::npmax(e, 0.0);
+    st[S_ECCI * n_pad + i] = Ecci0;
+    st[S_N * n_pad + i] = 0.0;
+    st[S_ALB * n_pad + i] = 0.3;
+  }
+}
+
+// materialise previous-step depths before a host overwrite of a depth field
+__global__ void k_materialise_depths(double* __restrict__ st, int64_t n_pad, double ws, double wi) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
+    st[S_HSNOW * n_pad + i] = st[S_HSWE * n_pad + i] * ws;
+    st[S_HICE * n_pad + i] = st[S_HIWE * n_pad + i] * wi;
+  }
+}
+
+template <class R>
+__global__ void k_check_slope(const R* __restrict__ slope, int64_t n, int32_t* __restrict__ flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    if (slope[i] < (R)0) atomicOr(flag, 1);
+}
+
+// --- synthetic workload (mirror: topoflow_glacier/synthetic.py) -----------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float hash_u01(uint64_t seed, uint64_t field, uint64_t frame, uint64_t cell) {
+  const uint64_t k = (field << 58) ^ (frame << 42) ^ cell;
+  return (float)(splitmix64(seed ^ splitmix64(k)) >> 40) * 0x1p-24f;
+}
+
+template <class R>
+__global__ void k_fill_synthetic(R* __restrict__ forc, R* __restrict__ stat, double* __restrict__ st,
+                                 int64_t n, int64_t n_pad, int64_t nx, int64_t row0, int64_t nx_global,
+                                 uint64_t seed, const float* __restrict__ diurnal, int n_frames) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nx, c = i % nx;
+    const uint64_t cell = (uint64_t)((row0 + r) * nx_global + c);
+    const float Tbar = -8.0f + 16.0f * hash_u01(seed, 6, 0, cell);
+    stat[i] = (R)(1500.0f + 1500.0f * hash_u01(seed, 7, 0, cell));
+    stat[n_pad + i] = (R)(0.5f + 99.5f * hash_u01(seed, 8, 0, cell));
+    stat[2 * n_pad + i] = (R)(360.0f * hash_u01(seed, 9, 0, cell));
+    const float h_swe = 0.25f * (0.8f + 0.4f * hash_u01(seed, 10, 0, cell));
+    const float h_iwe = 1.834f * (0.8f + 0.4f * hash_u01(seed, 11, 0, cell));
+    st[S_HSWE * n_pad + i] = (double)h_swe;
+    st[S_HIWE * n_pad + i] = (double)h_iwe;
+    st[S_HSNOW * n_pad + i] = (double)(h_swe * 20.0f);
+    st[S_HICE * n_pad + i] = (double)(h_iwe * 1.0905125f);
+    for (int f = 0; f < n_frames; ++f) {
+      R* fr = forc + (int64_t)f * kNumForc * n_pad;
+      const float T = (Tbar + 5.0f * diurnal[f]) + 2.0f * (hash_u01(seed, 0, f, cell) - 0.5f);
+      const float q = 0.0019f + 0.0042f * hash_u01(seed, 1, f, cell);
+      const float pa = 87100.0f + 2600.0f * hash_u01(seed, 2, f, cell);
+      const float uz = 0.28f + 15.5f * hash_u01(seed, 3, f, cell);
+      const float P = (hash_u01(seed, 4, f, cell) < 0.24f) ? 5.2e-7f * hash_u01(seed, 5, f, cell) : 0.0f;
+      fr[F_P * n_pad + i] = (R)P;
+      fr[F_T * n_pad + i] = (R)T;
+      fr[F_Q * n_pad + i] = (R)q;
+      fr[F_PA * n_pad + i] = (R)pa;
+      fr[F_UZ * n_pad + i] = (R)uz;
+    }
+  }
+}
+
+std::string g_err;  // errors before a handle exists
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+// ===========================================================================
+// Handle
+// ===========================================================================
+struct tfg_handle {
+  int device = 0, engine = TFG_F32;
+  int64_t ny = 0, nx = 0, n = 0, n_pad = 0;
+  int n_frames = 1, hist_depth = 1, n_catch = 1, ring_len = 72;
+  size_t rsz = 4;
+  DevParams dp{};
+  hipStream_t own_stream = nullptr, stream = nullptr;
+  void* forc = nullptr;
+  void* stat = nullptr;
+  void* lwsw = nullptr;          // [2][n_pad] R, not read by the physics
+  int32_t* catch_id = nullptr;
+  double* st = nullptr;
+  int64_t* tot = nullptr;
+  int32_t* ring = nullptr;
+  void* hist = nullptr;
+  double* diag = nullptr;        // [n_catch][6]
+  double* slab = nullptr;        // [max_blocks][n_catch][6]
+  float* d_diurnal = nullptr;
+  int32_t* d_flag = nullptr;
+  tfg_uniforms* d_u = nullptr;
+  int64_t d_u_cap = 0;
+  tfg_uniforms* h_u[2] = {nullptr, nullptr};
+  hipEvent_t h_u_ev[2] = {nullptr, nullptr};
+  int64_t h_u_cap[2] = {0, 0};
+  int h_u_next = 0;
+  void* staging = nullptr;
+  size_t staging_bytes = 0;
+  int max_blocks = 2048;
+  int fuse = 24;
+  bool depths_derived = false;
+  bool slope_invalid = false;
+  bool initialised = false;
+  int64_t last_hist = 0;
+  std::string err;
+};
+
+namespace {
+
+int fail(tfg_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg; else g_err = msg;
+  return code;
+}
+
+#define HIPCHK(h, call)                                                                  \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail((h), TFG_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+size_t dtype_size(int dt) { return dt == TFG_F64 ? 8 : 4; }
+
+int ensure_staging(tfg_handle* h, size_t bytes) {
+  if (bytes <= h->staging_bytes) return TFG_OK;
+  if (h->staging) HIPCHK(h, hipFree(h->staging));
+  h->staging = nullptr;
+  HIPCHK(h, hipMalloc(&h->staging, bytes));
+  h->staging_bytes = bytes;
+  return TFG_OK;
+}
+
+int grid_for(int64_t n) { return (int)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 8192); }
+
+// copy n elements of type st (host/device) into device buffer dst of type dt
+int upload(tfg_handle* h, void* dst, int dt, const void* src, int st, int64_t n, int on_dev) {
+  if (n <= 0) return TFG_OK;
+  const size_t sbytes = (size_t)n * dtype_size(st);
+  if (dt == st) {
+    HIPCHK(h, hipMemcpyAsync(dst, src, sbytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    if (!on_dev) HIPCHK(h, hipStreamSynchronize(h->stream));
+    return TFG_OK;
+  }
+  const void* dsrc = src;
+  if (!on_dev) {
+    int rc = ensure_staging(h, sbytes);
+    if (rc) return rc;
+    HIPCHK(h, hipMemcpyAsync(h->staging, src, sbytes, hipMemcpyHostToDevice, h->stream));
+    dsrc = h->staging;
+  }
+  const int gb = grid_for(n);
+  if (dt == TFG_F32 && st == TFG_F64)
+    hipLaunchKernelGGL((k_convert<float, double>), gb, 256, 0, h->stream, (float*)dst, (const double*)dsrc, n);
+  else if (dt == TFG_F64 && st == TFG_F32)
+    hipLaunchKernelGGL((k_convert<double, float>), gb, 256, 0, h->stream, (double*)dst, (const float*)dsrc, n);
+  else
+    return fail(h, TFG_ERR_ARG, "unsupported dtype conversion");
+  HIPCHK(h, hipGetLastError());
+  if (!on_dev) HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+int download(tfg_handle* h, void* dst, int dt, const void* src, int st, int64_t n, int on_dev) {
+  if (n <= 0) return TFG_OK;
+  const size_t dbytes = (size_t)n * dtype_size(dt);
+  const void* dsrc = src;
+  if (dt != st) {
+    void* conv = dst;
+    if (!on_dev) {
+      int rc = ensure_staging(h, dbytes);
+      if (rc) return rc;
+      conv = h->staging;
+    }
+    const int gb = grid_for(n);
+    if (dt == TFG_F32 && st == TFG_F64)
+      hipLaunchKernelGGL((k_convert<float, double>), gb, 256, 0, h->stream, (float*)conv, (const double*)src, n);
+    else if (dt == TFG_F64 && st == TFG_F32)
+      hipLaunchKernelGGL((k_convert<double, float>), gb, 256, 0, h->stream, (double*)conv, (const float*)src, n);
+    else
+      return fail(h, TFG_ERR_ARG, "unsupported dtype conversion");
+    HIPCHK(h, hipGetLastError());
+    if (on_dev) return TFG_OK;
+    dsrc = conv;
+  }
+  HIPCHK(h, hipMemcpyAsync(dst, dsrc, dbytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->stream));
+  if (!on_dev) HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+void derive_params(const tfg_params& q, DevParams& p) {
+  std::memset(&p, 0, sizeof(p));
+  const double pi = 3.141592653589793;
+  p.dt = q.dt;
+  p.da_m2 = q.da_m2;
+  p.T_rs = q.T_rain_snow;
+  p.dust = q.dust_atten;
+  p.F = q.canopy_factor;
+  p.one_minus_F_172 = (1.0 - q.canopy_factor) * 1.72;
+  p.cloud_term = 1.0 + (0.22 * (q.cloud_factor * q.cloud_factor));
+  p.rho_snow_Cp_snow = q.rho_snow * q.Cp_snow;
+  p.rho_air_Cp_air = q.rho_air * q.Cp_air;
+  p.rho_air_Lv = q.rho_air * q.Lv;
+  p.rho_H2O_Lf = q.rho_H2O * q.Lf;
+  p.lhc = q.latent_heat_constant;
+  p.sea_p0 = q.sea_level_p0;
+  p.negM_g = -q.M_mass_air * q.g;
+  p.R = q.uni_gas_const;
+  p.eps = q.eps;
+  p.one_minus_eps = 1.0 - q.eps;
+  p.z = 10.0;
+  p.gz = q.g * 10.0;
+  p.kappa = q.kappa;
+  p.z0 = q.z0_air;
+  p.sigma = q.sigma;
+  p.em_surf = q.em_surf;
+  p.em_surf_sigma = q.em_surf * q.sigma;
+  p.one_minus_em_surf = 1.0 - q.em_surf;
+  p.one_seventh = 1.0 / 7.0;
+  p.T0 = q.T0;
+  p.ws = q.rho_H2O / q.rho_snow;
+  p.wi = q.rho_H2O / q.rho_ice;
+  p.days_per_dt = q.dt / 86400.0;
+  p.pi_over_180 = pi / 180.0;
+  p.c180_over_pi = 180.0 / pi;
+  p.sin_lat = q.sin_lat;  // numpy values from the host (the reference computes them with numpy)
+  p.cos_lat = q.cos_lat;
+  {
+    // Ecci = max(((rho_ice*Cp_ice)*h_active_layer)*del_T, 0), del_T = T0 - 0  (:394-395)
+    const double e = (q.rho_ice * q.Cp_ice) * q.h_active_layer * (q.T0 - 0.0);
+    p.Ecci0 = (e >= 0.0 || e != e) ? e : 0.0;
+  }
+  p.omega = (360.0 / 24.0) * (pi / 180.0);
+  p.half_pi = pi / 2.0;
+  p.twopi = 2.0 * pi;
+  p.qscale = 68719476736.0;  // 2^36
+  p.thr_q = (int64_t)std::ceil(0.03 * 68719476736.0);
+  p.satterlund = q.satterlund;
+  p.ring_len = q.ring_len;
+  p.f_sea_p0 = (float)q.sea_level_p0;
+  p.f_negMg_over_R = (float)(p.negM_g / q.uni_gas_const);
+  p.f_eps = (float)q.eps;
+  p.f_one_minus_eps = (float)(1.0 - q.eps);
+  p.f_gz = (float)p.gz;
+  p.f_kappa = (float)q.kappa;
+  p.f_inv_z0 = (float)(1.0 / q.z0_air);
+  p.f_z = 10.0f;
+  p.f_rho_air_Cp_air = (float)p.rho_air_Cp_air;
+  p.f_rho_air_Lv = (float)p.rho_air_Lv;
+  p.f_lhc = (float)q.latent_heat_constant;
+  p.f_dust = (float)q.dust_atten;
+  p.f_F = (float)q.canopy_factor;
+  p.f_one_minus_F_172 = (float)p.one_minus_F_172;
+  p.f_cloud_term = (float)p.cloud_term;
+  p.f_em_surf_sigma = (float)p.em_surf_sigma;
+  p.f_sigma = (float)q.sigma;
+  p.f_one_minus_em_surf = (float)p.one_minus_em_surf;
+  p.f_inv_omega = (float)(1.0 / p.omega);
+  p.inv_dt = 1.0 / q.dt;
+  p.inv_dt_rhoLf = 1.0 / (q.dt * p.rho_H2O_Lf);
+  p.inv_z0 = 1.0 / q.z0_air;
+}
+
+void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {
+  const int64_t np = h->n_pad;
+  const size_t rs = h->rsz;
+  char* f = static_cast<char*>(h->forc);
+  char* hs = static_cast<char*>(h->hist);
+  switch (field) {
+    case TFG_IN_LW_IN: *dtype = h->engine; return static_cast<char*>(h->lwsw);
+    case TFG_IN_SW_IN: *dtype = h->engine; return static_cast<char*>(h->lwsw) + np * rs;
+    case TFG_IN_P: *dtype = h->engine; return f + ((int64_t)index * kNumForc + F_P) * np * rs;
+    case TFG_IN_T_AIR: *dtype = h->engine; return f + ((int64_t)index * kNumForc + F_T) * np * rs;
+    case TFG_IN_HUM_SP: *dtype = h->engine; return f + ((int64_t)index * kNumForc + F_Q) * np * rs;
+    case TFG_IN_P_AIR: *dtype = h->engine; return f + ((int64_t)index * kNumForc + F_PA) * np * rs;
+    case TFG_IN_UZ: *dtype = h->engine; return f + ((int64_t)index * kNumForc + F_UZ) * np * rs;
+    case TFG_OUT_H_SNOW: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_HSNOW) * np * rs;
+    case TFG_OUT_SM: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_SM) * np * rs;
+    case TFG_OUT_H_ICE: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_HICE) * np * rs;
+    case TFG_OUT_IM: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_IM) * np * rs;
+    case TFG_OUT_M_TOTAL: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_MTOT) * np * rs;
+    case TFG_OUT_RH: *dtype = h->engine; return hs + ((int64_t)index * kNumHist + H_RH) * np * rs;
+    case TFG_OUT_H_SWE: *dtype = TFG_F64; return h->st + S_HSWE * np;
+    case TFG_OUT_H_IWE: *dtype = TFG_F64; return h->st + S_HIWE * np;
+    case TFG_ST_ELEV: *dtype = h->engine; return static_cast<char*>(h->stat);
+    case TFG_ST_SLOPE: *dtype = h->engine; return static_cast<char*>(h->stat) + np * rs;
+    case TFG_ST_ASPECT: *dtype = h->engine; return static_cast<char*>(h->stat) + 2 * np * rs;
+    case TFG_ST_CATCH_ID: *dtype = TFG_I32; return h->catch_id;
+    case TFG_ST_ECCS: *dtype = TFG_F64; return h->st + S_ECCS * np;
+    case TFG_ST_ECCI: *dtype = TFG_F64; return h->st + S_ECCI * np;
+    case TFG_ST_ALBEDO: *dtype = TFG_F64; return h->st + S_ALB * np;
+    case TFG_ST_NDAYS: *dtype = TFG_F64; return h->st + S_N * np;
+    default: return nullptr;
+  }
+}
+
+bool is_frame_field(int f) { return f == TFG_IN_P || f == TFG_IN_T_AIR || f == TFG_IN_HUM_SP || f == TFG_IN_P_AIR || f == TFG_IN_UZ; }
+bool is_hist_field(int f) { return f == TFG_OUT_H_SNOW || f == TFG_OUT_SM || f == TFG_OUT_H_ICE || f == TFG_OUT_IM || f == TFG_OUT_M_TOTAL || f == TFG_OUT_RH; }
+
+template <class R, bool EXACT>
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds) {
+  KArgs a;
+  a.p = h->dp;
+  a.forc = h->forc;
+  a.stat = h->stat;
+  a.catch_id = h->catch_id;
+  a.st = h->st;
+  a.tot = h->tot;
+  a.ring = h->ring;
+  a.hist = h->hist;
+  a.slab = h->slab;
+  a.u = d_u;
+  a.K = K;
+  a.n_catch = h->n_catch;
+  a.n = h->n;
+  a.n_pad = h->n_pad;
+  const bool rd = !h->depths_derived;
+  const bool ct = h->catch_id != nullptr;
+  constexpr int C = kCellsPerThread;
+  if (rd && ct) hipLaunchKernelGGL((k_fused<R, EXACT, true, true, C>), blocks, kBlock, lds, h->stream, a);
+  else if (rd) hipLaunchKernelGGL((k_fused<R, EXACT, true, false, C>), blocks, kBlock, lds, h->stream, a);
+  else if (ct) hipLaunchKernelGGL((k_fused<R, EXACT, false, true, C>), blocks, kBlock, lds, h->stream, a);
+  else hipLaunchKernelGGL((k_fused<R, EXACT, false, false, C>), blocks, kBlock, lds, h->stream, a);
+  HIPCHK(h, hipGetLastError());
+  return TFG_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int tfg_abi_version(void) { return TFG_ABI_VERSION; }
+
+const char* tfg_build_info(void) {
+  return "libtfg abi=1 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
+         "k_diag_reduce, k_fill_synthetic";
+}
+
+int tfg_device_count(int* count) {
+  if (!count) return fail(nullptr, TFG_ERR_ARG, "null count");
+  HIPCHK(nullptr, hipGetDeviceCount(count));
+  return TFG_OK;
+}
+
+int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int device, int n_frames,
+               int hist_depth, int n_catch, tfg_handle** out) {
+  if (!p || !out) return fail(nullptr, TFG_ERR_ARG, "null params/out");
+  *out = nullptr;
+  if (ny <= 0 || nx <= 0) return fail(nullptr, TFG_ERR_ARG, "grid must have ny, nx >= 1");
+  if (engine != TFG_F32 && engine != TFG_F64) return fail(nullptr, TFG_ERR_ARG, "engine must be TFG_F32 or TFG_F64");
+  if (n_frames < 1 || hist_depth < 1 || n_catch < 1) return fail(nullptr, TFG_ERR_ARG, "n_frames, hist_depth, n_catch must be >= 1");
+  if (n_catch > 512) return fail(nullptr, TFG_ERR_ARG, "n_catch > 512 not supported");
+  if (p->ring_len < 1) return fail(nullptr, TFG_ERR_ARG, "ring_len must be >= 1");
+  if (!(p->dt > 0)) return fail(nullptr, TFG_ERR_ARG, "dt must be > 0");
+  tfg_handle* h = new (std::nothrow) tfg_handle();
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "out of host memory");
+  auto bail = [&](int rc) {
+    g_err = h->err;
+    tfg_destroy(h);
+    return rc;
+  };
+  h->device = device;
+  h->engine = engine;
+  h->rsz = dtype_size(engine);
+  h->ny = ny;
+  h->nx = nx;
+  h->n = ny * nx;
+  h->n_pad = round_up(h->n, 64);
+  h->n_frames = n_frames;
+  h->hist_depth = hist_depth;
+  h->n_catch = n_catch;
+  h->ring_len = p->ring_len;
+  derive_params(*p, h->dp);
+  if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TFG_ERR_HIP); }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) { h->err = "hipGetDeviceProperties failed"; return bail(TFG_ERR_HIP); }
+  h->max_blocks = std::max(256, prop.multiProcessorCount * 8);
+  if (const char* e = std::getenv("TFG_BLOCKS")) h->max_blocks = std::max(1, atoi(e));
+  if (const char* e = std::getenv("TFG_FUSE")) h->fuse = std::max(1, atoi(e));
+  if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "stream create failed"; return bail(TFG_ERR_HIP); }
+  h->stream = h->own_stream;
+  const int64_t np = h->n_pad;
+  const size_t rs = h->rsz;
+  struct A { void** p; size_t bytes; } allocs[] = {
+      {&h->forc, (size_t)n_frames * kNumForc * np * rs},
+      {&h->stat, 3 * (size_t)np * rs},
+      {&h->lwsw, 2 * (size_t)np * rs},
+      {(void**)&h->st, (size_t)kNumState * np * 8},
+      {(void**)&h->tot, (size_t)np * 8},
+      {(void**)&h->ring, (size_t)p->ring_len * np * 4},
+      {&h->hist, (size_t)hist_depth * kNumHist * np * rs},
+      {(void**)&h->diag, (size_t)n_catch * 6 * 8},
+      {(void**)&h->slab, (size_t)h->max_blocks * n_catch * 6 * 8},
+      {(void**)&h->d_flag, 4},
+  };
+  for (auto& a : allocs) {
+    hipError_t e = hipMalloc(a.p, a.bytes);
+    if (e != hipSuccess) {
+      h->err = std::string("hipMalloc(") + std::to_string(a.bytes) + " B) failed: " + hipGetErrorString(e);
+      return bail(TFG_ERR_HIP);
+    }
+    if (hipMemsetAsync(*a.p, 0, a.bytes, h->stream) != hipSuccess) { h->err = "hipMemset failed"; return bail(TFG_ERR_HIP); }
+  }
+  if (hipStreamSynchronize(h->stream) != hipSuccess) { h->err = "sync failed"; return bail(TFG_ERR_HIP); }
+  *out = h;
+  return TFG_OK;
+}
+
+int tfg_destroy(tfg_handle* h) {
+  if (!h) return TFG_OK;
+  hipSetDevice(h->device);
+  if (h->own_stream) hipStreamSynchronize(h->own_stream);
+  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag,
+                  h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
+  for (void* q : ptrs) if (q) hipFree(q);
+  for (int i = 0; i < 2; ++i) {
+    if (h->h_u[i]) hipHostFree(h->h_u[i]);
+    if (h->h_u_ev[i]) hipEventDestroy(h->h_u_ev[i]);
+  }
+  if (h->own_stream) hipStreamDestroy(h->own_stream);
+  delete h;
+  return TFG_OK;
+}
+
+int tfg_set_stream(tfg_handle* h, void* stream) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+  return TFG_OK;
+}
+
+int tfg_get_stream(tfg_handle* h, void** stream) {
+  if (!h || !stream) return fail(h, TFG_ERR_ARG, "null argument");
+  *stream = h->stream;
+  return TFG_OK;
+}
+
+int tfg_set_fuse(tfg_handle* h, int k) {
+  if (!h || k < 1) return fail(h, TFG_ERR_ARG, "fuse must be >= 1");
+  h->fuse = k;
+  return TFG_OK;
+}
+
+int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_dtype, int64_t n,
+                  int src_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!src) return fail(h, TFG_ERR_ARG, "null src");
+  if (n != h->n) return fail(h, TFG_ERR_ARG, "n = " + std::to_string(n) + " != ny*nx = " + std::to_string(h->n));
+  HIPCHK(h, hipSetDevice(h->device));
+  if (is_frame_field(field) && (index < 0 || index >= h->n_frames)) return fail(h, TFG_ERR_ARG, "frame index out of range");
+  if (is_hist_field(field) && (index < 0 || index >= h->hist_depth)) return fail(h, TFG_ERR_ARG, "history slot out of range");
+  if (field == TFG_ST_CATCH_ID) {
+    if (src_dtype != TFG_I32) return fail(h, TFG_ERR_ARG, "catchment ids must be TFG_I32");
+    if (!h->catch_id) {
+      HIPCHK(h, hipMalloc((void**)&h->catch_id, (size_t)h->n_pad * 4));
+      HIPCHK(h, hipMemsetAsync(h->catch_id, 0, (size_t)h->n_pad * 4, h->stream));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->catch_id, src, (size_t)n * 4, src_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+    std::vector<int32_t> tmp;
+    const int32_t* hs = static_cast<const int32_t*>(src);
+    if (src_on_device) {
+      tmp.resize(n);
+      HIPCHK(h, hipMemcpyAsync(tmp.data(), src, (size_t)n * 4, hipMemcpyDeviceToHost, h->stream));
+      hs = tmp.data();
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (int64_t i = 0; i < n; ++i)
+      if (hs[i] < 0 || hs[i] >= h->n_catch) return fail(h, TFG_ERR_ARG, "catchment id out of [0, n_catch)");
+    return TFG_OK;
+  }
+  if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  int fdt = 0;
+  void* dst = field_ptr(h, field, index, &fdt);
+  if (!dst) return fail(h, TFG_ERR_ARG, "unknown field id " + std::to_string(field));
+  const bool depth = field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE || field == TFG_OUT_H_SWE || field == TFG_OUT_H_IWE;
+  if (depth && h->depths_derived) {
+    // keep the previous-step depths the next update() must see (:895-911)
+    hipLaunchKernelGGL(k_materialise_depths, grid_for(h->n_pad), 256, 0, h->stream, h->st, h->n_pad, h->dp.ws, h->dp.wi);
+    HIPCHK(h, hipGetLastError());
+    h->depths_derived = false;
+  }
+  if (field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE) {
+    // user-set depth: both the fp64 state and the visible output
+    double* sd = h->st + (field == TFG_OUT_H_SNOW ? S_HSNOW : S_HICE) * h->n_pad;
+    int rc = upload(h, sd, TFG_F64, src, src_dtype, n, src_on_device);
+    if (rc) return rc;
+    return upload(h, dst, fdt, src, src_dtype, n, src_on_device);
+  }
+  int rc = upload(h, dst, fdt, src, src_dtype, n, src_on_device);
+  if (rc) return rc;
+  if (field == TFG_ST_SLOPE) {
+    HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
+    if (h->engine == TFG_F32)
+      hipLaunchKernelGGL((k_check_slope<float>), grid_for(n), 256, 0, h->stream, (const float*)dst, n, h->d_flag);
+    else
+      hipLaunchKernelGGL((k_check_slope<double>), grid_for(n), 256, 0, h->stream, (const double*)dst, n, h->d_flag);
+    int32_t flag = 0;
+    HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->slope_invalid = flag != 0;
+    if (flag) return fail(h, TFG_ERR_DOMAIN, "ERROR: some slope angles are out of range (beta not in [0, pi/2]; bmi_topoflow_glacier.py:1106-1111)");
+  }
+  return TFG_OK;
+}
+
+int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
+  if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (is_frame_field(field) && (index < 0 || index >= h->n_frames)) return fail(h, TFG_ERR_ARG, "frame index out of range");
+  if (is_hist_field(field) && (index < 0 || index >= h->hist_depth)) return fail(h, TFG_ERR_ARG, "history slot out of range");
+  if (field == TFG_ST_CATCH_ID) {
+    if (dst_dtype != TFG_I32) return fail(h, TFG_ERR_ARG, "catchment ids are TFG_I32");
+    if (!h->catch_id) return fail(h, TFG_ERR_STATE, "no catchment-id raster set");
+    HIPCHK(h, hipMemcpyAsync(dst, h->catch_id, (size_t)n * 4, dst_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return TFG_OK;
+  }
+  if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+  int fdt = 0;
+  const void* src = field_ptr(h, field, index, &fdt);
+  if (!src) return fail(h, TFG_ERR_ARG, "unknown field id " + std::to_string(field));
+  if ((field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE) && !h->depths_derived) {
+    // before any step (or right after a host set) the depths live in the fp64 state
+    src = h->st + (field == TFG_OUT_H_SNOW ? S_HSNOW : S_HICE) * h->n_pad;
+    fdt = TFG_F64;
+  }
+  return download(h, dst, dst_dtype, src, fdt, n, dst_on_device);
+}
+
+int tfg_init_state(tfg_handle* h) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  HIPCHK(h, hipSetDevice(h->device));
+  const DevParams& p = h->dp;
+  // Eccs = max((rho_snow*Cp_snow)*h_snow*del_T, 0); del_T = T0 - T_surf(=0)  (:389-395)
+  const double del_T = p.T0 - 0.0;
+  hipLaunchKernelGGL(k_init_state, grid_for(h->n_pad), 256, 0, h->stream, h->st, h->n_pad, p.rho_snow_Cp_snow, del_T, p.Ecci0);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemsetAsync(h->tot, 0, (size_t)h->n_pad * 8, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->ring, 0, (size_t)h->ring_len * h->n_pad * 4, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->hist, 0, (size_t)h->hist_depth * kNumHist * h->n_pad * h->rsz, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->diag, 0, (size_t)h->n_catch * 6 * 8, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->depths_derived = false;
+  h->initialised = true;
+  return TFG_OK;
+}
+
+int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (nsteps <= 0) return TFG_OK;
+  if (!u) return fail(h, TFG_ERR_ARG, "null uniforms");
+  if (!h->initialised) return fail(h, TFG_ERR_STATE, "tfg_init_state() has not been called");
+  if (h->slope_invalid) return fail(h, TFG_ERR_DOMAIN, "slope raster invalid (bmi_topoflow_glacier.py:1106-1111)");
+  for (int64_t k = 0; k < nsteps; ++k) {
+    if (u[k].frame < 0 || u[k].frame >= h->n_frames) return fail(h, TFG_ERR_ARG, "uniforms: frame out of range");
+    if (u[k].hist < 0 || u[k].hist >= h->hist_depth) return fail(h, TFG_ERR_ARG, "uniforms: hist slot out of range");
+    if (u[k].slot < 0 || u[k].slot >= h->ring_len) return fail(h, TFG_ERR_ARG, "uniforms: ring slot out of range");
+  }
+  HIPCHK(h, hipSetDevice(h->device));
+  // stage uniforms: pinned double buffer -> device array
+  const int b = h->h_u_next;
+  h->h_u_next ^= 1;
+  if (h->h_u_ev[b]) HIPCHK(h, hipEventSynchronize(h->h_u_ev[b]));
+  else HIPCHK(h, hipEventCreateWithFlags(&h->h_u_ev[b], hipEventDisableTiming));
+  if (h->h_u_cap[b] < nsteps) {
+    if (h->h_u[b]) HIPCHK(h, hipHostFree(h->h_u[b]));
+    h->h_u[b] = nullptr;
+    HIPCHK(h, hipHostMalloc((void**)&h->h_u[b], (size_t)nsteps * sizeof(tfg_uniforms), hipHostMallocDefault));
+    h->h_u_cap[b] = nsteps;
+  }
+  if (h->d_u_cap < nsteps) {
+    // the previous launches may still read d_u: wait before reallocating
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->d_u) HIPCHK(h, hipFree(h->d_u));
+    h->d_u = nullptr;
+    HIPCHK(h, hipMalloc((void**)&h->d_u, (size_t)nsteps * sizeof(tfg_uniforms)));
+    h->d_u_cap = nsteps;
+  }
+  std::memcpy(h->h_u[b], u, (size_t)nsteps * sizeof(tfg_uniforms));
+  HIPCHK(h, hipMemcpyAsync(h->d_u, h->h_u[b], (size_t)nsteps * sizeof(tfg_uniforms), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipEventRecord(h->h_u_ev[b], h->stream));
+
+  const int64_t ngroups = h->n_pad / kCellsPerThread;
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
+  const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
+  const int nb = h->n_catch * 6;
+  for (int64_t k0 = 0; k0 < nsteps; k0 += h->fuse) {
+    const int K = (int)std::min<int64_t>(h->fuse, nsteps - k0);
+    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, h->d_u + k0, K, blocks, lds)
+                                    : launch_fused<double, true>(h, h->d_u + k0, K, blocks, lds);
+    if (rc) return rc;
+    h->depths_derived = true;
+    hipLaunchKernelGGL(k_diag_reduce, nb, kBlock, 0, h->stream, h->slab, blocks, nb, h->diag);
+    HIPCHK(h, hipGetLastError());
+  }
+  h->last_hist = u[nsteps - 1].hist;
+  return TFG_OK;
+}
+
+int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
+  if (!h || !out) return fail(h, TFG_ERR_ARG, "null argument");
+  if (n_catch != h->n_catch) return fail(h, TFG_ERR_ARG, "n_catch mismatch");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemcpyAsync(out, h->diag, (size_t)n_catch * 6 * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  // P_max of an empty history is 0 like the reference's initial P_max (:314)
+  for (int c = 0; c < n_catch; ++c) if (out[c * 6 + 5] == -INFINITY) out[c * 6 + 5] = 0.0;
+  return TFG_OK;
+}
+
+int tfg_reset_diag(tfg_handle* h) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipMemsetAsync(h->diag, 0, (size_t)h->n_catch * 6 * 8, h->stream));
+  return TFG_OK;
+}
+
+int tfg_sync(tfg_handle* h) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_global, const float* diurnal,
+                       int n_frames) {
+  if (!h || !diurnal) return fail(h, TFG_ERR_ARG, "null argument");
+  if (n_frames != h->n_frames) return fail(h, TFG_ERR_ARG, "n_frames mismatch");
+  if (nx_global != h->nx) return fail(h, TFG_ERR_ARG, "row-block shards must span full rows (nx_global == nx)");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (!h->d_diurnal) HIPCHK(h, hipMalloc((void**)&h->d_diurnal, (size_t)n_frames * 4));
+  HIPCHK(h, hipMemcpyAsync(h->d_diurnal, diurnal, (size_t)n_frames * 4, hipMemcpyHostToDevice, h->stream));
+  const int gb = grid_for(h->n);
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_fill_synthetic<float>), gb, 256, 0, h->stream, (float*)h->forc, (float*)h->stat, h->st,
+                       h->n, h->n_pad, h->nx, row0, nx_global, seed, h->d_diurnal, n_frames);
+  else
+    hipLaunchKernelGGL((k_fill_synthetic<double>), gb, 256, 0, h->stream, (double*)h->forc, (double*)h->stat, h->st,
+                       h->n, h->n_pad, h->nx, row0, nx_global, seed, h->d_diurnal, n_frames);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->slope_invalid = false;
+  return tfg_init_state(h);
+}
+
+const char* tfg_last_error(const tfg_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+}  // extern "C"

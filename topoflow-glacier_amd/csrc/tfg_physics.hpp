@@ -1,0 +1,531 @@
+// tfg_physics.hpp -- per-cell glacier energy balance, device side (gfx950).
+//
+// One call of cell_step_* advances ONE cell by ONE time step: the body of
+// BmiTopoflowGlacier.update() (bmi_topoflow_glacier.py:413-465) after the
+// per-step uniform scalars have been hoisted to the host (tfg_uniforms).
+//
+// Two variants share the state layout:
+//   cell_step_exact  fp64 everywhere, the reference's operation order, FMA
+//                    contraction off.  Used for single-catchment BMI runs
+//                    (float64 BMI surface, golden parity ~1e-13).
+//   cell_step_fast   fp32 forcing/static/outputs and fp32 flux arithmetic,
+//                    fp64 state update (cold contents, SWE/IWE, integrals) and
+//                    fp64 evaluation of the discontinuity predicates (rain/snow
+//                    split, depth tests, dark mask near sunrise/sunset).
+//
+// Elementwise rules for the reference's scalar-only branches:
+// bot==0 (:642), T_air==T_surf / Ri>0 (:672-726), dark (SF:939-941) are
+// evaluated per cell.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tfg {
+
+// ---------------------------------------------------------------------------
+// Constants derived on the host (fp64) from tfg_params, in the reference's
+// association order where it matters.
+// ---------------------------------------------------------------------------
+struct DevParams {
+  double dt, da_m2, T_rs, dust, F, one_minus_F_172, cloud_term;
+  double rho_snow_Cp_snow;    // (rho_snow*Cp_snow)               :1533
+  double rho_air_Cp_air;      // (rho_air*Cp_air)                 :745
+  double rho_air_Lv;          // rho_air*Lv                        :932
+  double rho_H2O_Lf;          // (rho_H2O*Lf)                      :1368
+  double lhc;                 // latent_heat_constant              :931
+  double sea_p0, negM_g, R;   // -M*g, R_star                      :552
+  double eps, one_minus_eps;  // :817
+  double gz;                  // g*z (z = 10 m)                    :640
+  double z, kappa, z0;        // :670
+  double em_surf_sigma, sigma, one_minus_em_surf, em_surf;
+  double one_seventh;         // np.float64(1)/7                   :292
+  double T0;                  // T0_cc                             :389
+  double Ecci0;               // initial ice cold content          :394-395
+  double inv_dt, inv_dt_rhoLf, inv_z0;  // reciprocals for the fast variant
+  double ws, wi;              // rho_H2O/rho_snow, rho_H2O/rho_ice :385-386
+  double days_per_dt;         // dt/86400                          :287
+  double sin_lat, cos_lat;    // of lat*(pi/180)                   SF:730-733
+  double omega;               // Earth_Angular_Velocity()          SF:252
+  double pi_over_180, c180_over_pi, half_pi, twopi;
+  double qscale;              // 2^36: snowfall-window fixed point
+  int64_t thr_q;              // ceil(0.03 * 2^36)                 :1040
+  int32_t satterlund;
+  int32_t ring_len;
+  // fp32 copies used by the fast variant
+  float f_sea_p0, f_negMg_over_R, f_eps, f_one_minus_eps, f_gz, f_kappa, f_inv_z0, f_z;
+  float f_rho_air_Cp_air, f_rho_air_Lv, f_lhc, f_dust, f_F, f_one_minus_F_172, f_cloud_term;
+  float f_em_surf_sigma, f_sigma, f_one_minus_em_surf, f_inv_omega;
+};
+
+// Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
+// :1082-1093, set_slope_angle :1095-1113, Equivalent_Latitude SF:741,
+// Longitude_Offset SF:718, Noon_Offset_Slope SF:772).
+struct CellStatic {
+  double elev;
+  double cos_leq, sin_leq;  // of lat_eq [rad]                      SF:866-868
+  double dlon;              // Longitude_Offset [rad]                SF:864
+  double tan_eq;            // tan(eq_lat_deg*(pi/180))             SF:325
+  double t_noon;            // Noon_Offset_Slope [h]                 SF:776
+};
+
+// Per-cell model state carried between steps (fp64).
+struct CellState {
+  double h_swe, h_iwe, Eccs, Ecci, n, albedo;
+  double h_snow, h_ice;     // previous-step depths
+  int64_t tot_q;            // snowfall-window running total, fixed point
+};
+
+struct CellOut {
+  double h_snow, SM, h_ice, IM, M_total, RH;
+};
+
+struct CellDiag {
+  double P, PR, PS, SM, IM, Pmax;
+};
+
+// numpy np.maximum / np.minimum: NaN-propagating
+template <class R> __device__ __forceinline__ R npmax(R a, R b) { return (a >= b || a != a) ? a : b; }
+template <class R> __device__ __forceinline__ R npmin(R a, R b) { return (a <= b || a != a) ? a : b; }
+
+// numpy float remainder (npy_divmod) for b > 0
+__device__ __forceinline__ double pyremainder(double a, double b) {
+  double m = fmod(a, b);
+  if (m != 0.0) {
+    if ((b < 0.0) != (m < 0.0)) m += b;
+  } else {
+    m = copysign(0.0, b);
+  }
+  return m;
+}
+
+// Snowfall-window slot value in fixed point (2^-36 quantum, saturating).
+// The reference keeps a ring of int(72/dt) float64 values and re-sums it each
+// step (:1027-1041); only the predicate sum >= 0.03 is used.  A fixed-point
+// running total decides it exactly up to ring_len*2^-37 (< 2.2e-9 at 288
+// slots), with no drift.
+__device__ __forceinline__ int32_t window_q(double v, double qscale) {
+  double s = v * qscale;
+  if (!(s == s)) return 0;
+  if (s > 2147483647.0) return 2147483647;
+  if (s < -2147483647.0) return -2147483647;
+  return (int32_t)__double2ll_rn(s);
+}
+
+// ---------------------------------------------------------------------------
+// Static derivation (once per launch per cell).
+// ---------------------------------------------------------------------------
+__device__ inline CellStatic derive_static(const DevParams& p, double elev, double slope, double aspect) {
+#pragma clang fp contract(off)
+  CellStatic s;
+  s.elev = elev;
+  // set_aspect_angle (:1086-1091): aspect in DEGREES used as radians (quirk)
+  double alpha = p.half_pi - aspect;
+  alpha = pyremainder(p.twopi + alpha, p.twopi);
+  if (!isfinite(alpha)) alpha = 0.0;
+  // set_slope_angle (:1099-1104); out-of-range beta is rejected at upload
+  double beta = atan(slope);
+  beta = pyremainder(p.twopi + beta, p.twopi);
+  if (!isfinite(beta)) beta = 0.0;
+  const double sb = sin(beta), cb = cos(beta), sa = sin(alpha), ca = cos(alpha);
+  // Equivalent_Latitude SF:753-757
+  const double t1 = sb * ca * p.cos_lat;
+  const double t2 = cb * p.sin_lat;
+  const double lat_eq = asin(t1 + t2);
+  // Longitude_Offset SF:730-734
+  const double u1 = sb * sa;
+  const double u2 = cb * p.cos_lat;
+  const double u3 = sb * p.sin_lat * ca;
+  const double dlon = atan(u1 / (u2 - u3));
+  s.dlon = dlon;
+  s.t_noon = -1.0 * dlon / p.omega;  // SF:776
+  s.cos_leq = cos(lat_eq);
+  s.sin_leq = sin(lat_eq);
+  // Sunrise_Offset(eq_lat_deg, ...) SF:320-325: degrees and back
+  const double eq_lat_deg = lat_eq * p.c180_over_pi;
+  s.tan_eq = tan(eq_lat_deg * p.pi_over_180);
+  return s;
+}
+
+// Sunrise/sunset offsets on the slope (SF:783-830), fp64.
+__device__ __forceinline__ void slope_sun_offsets(const DevParams& p, const CellStatic& s, double tan_d,
+                                                  double flat_sr, double flat_ss, double& T_sr,
+                                                  double& T_ss) {
+#pragma clang fp contract(off)
+  double arg = -1.0 * s.tan_eq * tan_d;
+  arg = npmin(npmax(-1.0, arg), 1.0);
+  const double ac = acos(arg);
+  const double t_sr = -1.0 * ac / p.omega;
+  const double t_ss = ac / p.omega;
+  T_sr = npmax(t_sr + s.t_noon, flat_sr);
+  T_ss = npmin(t_ss + s.t_noon, flat_ss);
+}
+
+// ---------------------------------------------------------------------------
+// State update after the net energy flux (fp64, reference order).
+// :1566-1731 -- shared by both variants.
+// ---------------------------------------------------------------------------
+template <bool FAST>
+__device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, double P_snow,
+                                              double P_rain, double RH, double T_wb,
+                                              CellState& st, CellOut& o,
+                                              CellDiag& d, bool valid) {
+#pragma clang fp contract(off)
+  const double dt = p.dt;
+  const double previous_swe = st.h_swe;  // :1566-1571
+  // update_snow_meltrate :1364-1373
+  double E_in = Q_sum * dt;
+  double E_rem = npmax(E_in - st.Eccs, 0.0);
+  // FAST: value-only divisions become products with host reciprocals; the
+  // divisions that decide melt-out residuals (t/3600 below) stay exact.
+  double SM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
+  // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
+  // min(SM, h_swe/dt) lines are inside the method's docstring.
+  SM = npmax(SM, 0.0);
+  // update_SM_integral :1486
+  if (valid) d.SM += SM * p.da_m2 * dt * 3600.0;
+  // update_swe :1594-1606
+  double h_swe = st.h_swe + P_snow * dt;
+  double t = npmin(SM * 3600.0, h_swe);
+  SM = t / 3600.0;
+  h_swe = h_swe - SM * dt * 3600.0;
+  h_swe = npmax(h_swe, 0.0);
+  // update_snowfall_cold_content :1507-1537
+  double Eccs = st.Eccs;
+  if (P_snow > 0.0) {
+    const double new_h_snow = (P_snow * dt) * p.ws;
+    const double del_T = p.T0 - T_wb;
+    Eccs = npmax(Eccs + p.rho_snow_Cp_snow * new_h_snow * del_T - E_in, 0.0);
+  }
+  // update_ice_meltrate :1418-1434
+  E_rem = npmax(E_in - st.Ecci, 0.0);
+  double IM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
+  IM = npmax(IM, 0.0);
+  IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
+  double Ecci = npmax(st.Ecci - E_in, 0.0);
+  Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;  // previous-step h_ice
+  // enforce_max_ice_meltrate :1473-1480
+  IM = npmin(IM, FAST ? st.h_iwe * p.inv_dt : st.h_iwe / dt);
+  IM = npmax(IM, 0.0);
+  // update_IM_integral :1493
+  if (valid) d.IM += IM * p.da_m2 * dt * 3600.0;
+  // update_iwe :1612-1617
+  t = npmin(IM * 3600.0, st.h_iwe);
+  IM = t / 3600.0;
+  double h_iwe = st.h_iwe - IM * dt * 3600.0;
+  h_iwe = npmax(h_iwe, 0.0);
+  // update_combined_meltrate :1441-1443
+  const double M_total = IM + SM + (FAST ? P_rain * (1.0 / 3600.0) : P_rain / 3600.0);
+  // update_snow_depth :1711 / update_ice_depth :1726
+  const double h_snow = h_swe * p.ws;
+  const double h_ice = h_iwe * p.wi;
+  // update_snowpack_cold_content :1556-1558 (new h_snow)
+  Eccs = (P_snow <= 0.0) ? npmax(Eccs - E_in, 0.0) : Eccs;
+  Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
+
+  st.h_swe = h_swe;
+  st.h_iwe = h_iwe;
+  st.Eccs = Eccs;
+  st.Ecci = Ecci;
+  st.h_snow = h_snow;
+  st.h_ice = h_ice;
+  o.h_snow = h_snow;
+  o.h_ice = h_ice;
+  o.SM = SM;
+  o.IM = IM;
+  o.M_total = M_total;
+  o.RH = RH;
+}
+
+// Albedo ageing (:1020-1059) given the window predicate.
+__device__ __forceinline__ double albedo_exp(double x) { return exp(x); }
+__device__ __forceinline__ float albedo_exp(float x) { return __expf(x); }
+
+template <class R>
+__device__ __forceinline__ R albedo_step(const DevParams& p, CellState& st, bool wet_window, R T_air) {
+  // n: where(tot >= .03, 0, n); where(tot < .03, n + days_per_dt, n)
+  st.n = wet_window ? 0.0 : st.n + p.days_per_dt;
+  const R r = (T_air > (R)0) ? (R)0.12 : (R)0.05;
+  const R snow_albedo = (R)0.4 + (R)0.44 * albedo_exp((R)(-st.n) * r);
+  double albedo = (st.h_snow > 0.0) ? (double)snow_albedo : st.albedo;
+  if (st.h_snow == 0.0 && st.h_ice > 0.0) albedo = 0.3;
+  if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
+  st.albedo = albedo;
+  return (R)albedo;
+}
+
+
+// ---------------------------------------------------------------------------
+// EXACT variant (fp64, reference order)
+// ---------------------------------------------------------------------------
+__device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
+                                       double P, double T_air, double Hum_sp, double P_air, double uz,
+                                       int32_t q_old, int32_t& q_new, CellState& st, CellOut& o,
+                                       CellDiag& d, bool valid) {
+#pragma clang fp contract(off)
+  const double dt = p.dt;
+  const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
+  // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556
+  const double T_K = T_air + 273.15;
+  double p0 = p.sea_p0 * exp(p.negM_g * s.elev / (p.R * T_K));
+  p0 = p0 / 1000.0;
+  p0 = p0 * 10.0;
+  // :567, :576, :585, :604, :613, :623
+  const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
+  const double P_snow = P * ((T_air <= p.T_rs) ? 1.0 : 0.0);
+  if (valid) {
+    d.P += P * p.da_m2 * dt;
+    d.Pmax = npmax(d.Pmax, P);
+    d.PR += P_rain * p.da_m2 * dt;
+    d.PS += P_snow * p.da_m2 * dt;
+  }
+  // saturation vapour pressure (air) :788-802
+  double e_sat_air;
+  if (!p.satterlund) {
+    e_sat_air = 0.611 * exp((17.3 * T_air) / (T_air + 237.3));
+  } else {
+    e_sat_air = pow(10.0, 11.4 - 2353.0 / (T_air + 273.15)) / 1000.0;
+  }
+  e_sat_air = e_sat_air * 10.0;
+  // :817-826
+  double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
+  e = e / 1000.0;
+  const double e_air = e * 10.0;
+  const double RH = e_air / e_sat_air;  // :838
+  // :888-893
+  const double log_term = log(e_air / 6.1121);
+  const double T_dew = 257.14 * log_term / (18.678 - log_term);
+  // :906-910 (previous-step depths)
+  const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
+  double e_sat_surf;
+  if (!p.satterlund) {
+    e_sat_surf = 0.611 * exp((17.3 * T_surf) / (T_surf + 237.3));
+  } else {
+    e_sat_surf = pow(10.0, 11.4 - 2353.0 / (T_surf + 273.15)) / 1000.0;
+  }
+  e_sat_surf = e_sat_surf * 10.0;
+  // :640-644, per cell
+  const double top = p.gz * (T_air - T_surf);
+  double bot = (uz * uz) * (T_air + 273.15);
+  if (bot == 0.0) bot = 0.01;
+  const double Ri = top / bot;
+  // :670-726
+  const double arg = p.kappa / log(npmax((p.z - h_snow) / p.z0, 0.01));
+  const double Dn = uz * (arg * arg);
+  const double Dh = (Ri > 0.0) ? Dn / (1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  // :744-745
+  const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
+  // :919-920
+  const double W_p = 1.12 * exp(0.0614 * T_dew);
+  // :853 (SURFACE uses the air RH)
+  const double e_surf = RH * e_sat_surf;
+  // :931-934
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
+  // albedo :1023-1059 with the fixed-point window
+  q_new = window_q(P_snow * dt * p.ws, p.qscale);
+  st.tot_q += (int64_t)q_new - (int64_t)q_old;
+  const double albedo = albedo_step<double>(p, st, st.tot_q >= p.thr_q, T_air);
+  // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
+  const double a_sa = -0.1240 - (0.0207 * W_p);
+  const double b_sa = -0.0682 - (0.0248 * W_p);
+  const double tau = npmin(npmax(exp(a_sa + (b_sa * u.m_opt)) - p.dust, 0.0), 1.0);
+  double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos(u.omega_th + s.dlon) + s.sin_leq * u.sin_d);
+  K_ET = npmax(K_ET, 0.0);
+  const double a_s = -0.0363 - (0.0084 * W_p);
+  const double b_s = -0.0572 - (0.0173 * W_p);
+  const double gam_s = (1.0 - exp(a_s + (b_s * u.m_opt))) + p.dust;
+  const double K_dif = 0.5 * gam_s * u.k_et_flat;
+  const double K_global = tau * u.k_et_flat + K_dif;
+  const double K_bs = 0.5 * gam_s * albedo * K_global;
+  double K_cs = (tau * K_ET) + K_dif + K_bs;
+  double T_sr, T_ss;
+  slope_sun_offsets(p, s, u.tan_d, u.flat_sr, u.flat_ss, T_sr, T_ss);
+  if ((u.th <= T_sr) || (u.th >= T_ss)) K_cs = 0.0;
+  const double Qn_SW = K_cs * (1.0 - albedo);  // :1139
+  // update_em_air :1167-1192
+  const double T_air_K = T_air + 273.15;
+  double em_air;
+  if (!p.satterlund) {
+    const double term1 = p.one_minus_F_172 * pow((e_air / 10.0) / T_air_K, p.one_seventh);
+    em_air = (term1 * p.cloud_term) + p.F;
+  } else {
+    em_air = 1.08 * (1.0 - exp(-1.0 * pow(e_air, T_air_K / 2016.0)));
+  }
+  // :1231-1248
+  const double T_surf_K = T_surf + 273.15;
+  const double LW_in = em_air * p.sigma * pow(T_air_K, 4.0);
+  double LW_out = p.em_surf_sigma * pow(T_surf_K, 4.0);
+  LW_out = LW_out + p.one_minus_em_surf * LW_in;
+  const double Qn_LW = LW_in - LW_out;
+  // :1314 (Qa = Qc = 0)
+  const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + 0.0;
+  // Stull wet bulb (:1514-1520), only needed where it snows
+  double T_wb = 0.0;
+  if (P_snow > 0.0) {
+    T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
+           ((0.00391838 * pow(RH, 1.5)) * atan(0.023101 * RH)) - 4.86035;
+  }
+  melt_and_mass<false>(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
+}
+
+// ---------------------------------------------------------------------------
+// FAST variant: fp32 fluxes, fp64 state and predicates
+// ---------------------------------------------------------------------------
+struct CellStaticF {
+  float elev, cos_leq, sin_leq, cos_dlon, sin_dlon, t_noon_f, tan_eq_f;
+  double tan_eq, t_noon;  // fp64 copies for the near-edge dark test
+};
+
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float fexp(float x) { return fexp2(x * 1.4426950408889634f); }
+__device__ __forceinline__ float flog(float x) { return flog2(x) * 0.6931471805599453f; }
+
+// fp32 solar geometry of a cell (from derive_static, once per launch)
+__device__ inline CellStaticF derive_static_f(const DevParams& p, double elev, double slope, double aspect) {
+  double sa, ca;
+  sincos(aspect, &ca, &sa);
+  if (!isfinite(sa) || !isfinite(ca)) { sa = 1.0; ca = 0.0; }
+  double sb, cb;
+  if (!(slope == slope)) { sb = 0.0; cb = 1.0; }
+  else if (isinf(slope)) { sb = 1.0; cb = 0.0; }
+  else { const double r = 1.0 / sqrt(1.0 + slope * slope); sb = slope * r; cb = r; }
+  const double sl = sb * ca * p.cos_lat + cb * p.sin_lat;
+  const double cl = sqrt(fmax(1.0 - sl * sl, 0.0));
+  const double t = (sb * sa) / (cb * p.cos_lat - sb * p.sin_lat * ca);
+  const double rt = 1.0 / sqrt(1.0 + t * t);
+  CellStaticF f;
+  f.elev = (float)elev;
+  f.sin_leq = (float)sl;
+  f.cos_leq = (float)cl;
+  f.cos_dlon = (float)rt;
+  f.sin_dlon = (float)(t * rt);
+  f.t_noon = -1.0 * atan(t) / p.omega;
+  f.tan_eq = sl / cl;
+  f.t_noon_f = (float)f.t_noon;
+  f.tan_eq_f = (float)f.tan_eq;
+  return f;
+}
+
+// Dark test in fp64 (SF:939) for a cell whose fp32 estimate lies within
+// 0.02 h of sunrise/sunset: the reference's Sunrise/Sunset_Offset_Slope in
+// fp64 from the cell's fp64 tan(eq_lat) and noon offset.
+__device__ __noinline__ bool dark_exact(const DevParams& p, double tan_eq, double t_noon,
+                                        const tfg_uniforms* __restrict__ up) {
+#pragma clang fp contract(off)
+  double arg = -1.0 * tan_eq * up->tan_d;
+  arg = npmin(npmax(-1.0, arg), 1.0);
+  const double ac = acos(arg);
+  const double T_sr = npmax(-1.0 * ac / p.omega + t_noon, up->flat_sr);
+  const double T_ss = npmin(ac / p.omega + t_noon, up->flat_ss);
+  return (up->th <= T_sr) || (up->th >= T_ss);
+}
+
+__device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf, const tfg_uniforms* __restrict__ up,
+                                      const tfg_uniforms& u, float P, float T_air, float Hum_sp,
+                                      float P_air, float uz, int32_t q_old, int32_t& q_new,
+                                      CellState& st, CellOut& o, CellDiag& d, bool valid) {
+  const double dt = p.dt;
+  const double h_snow = st.h_snow, h_ice = st.h_ice;
+  const float T_K = T_air + 273.15f;
+  // p0 [mbar] = sea_p0 * exp(-M g elev / (R T_K)) / 100
+  const float p0 = p.f_sea_p0 * 0.01f * fexp(p.f_negMg_over_R * sf.elev * frcp(T_K));
+  const double Pd = (double)P;
+  const double Td = (double)T_air;
+  const bool is_rain = Td > p.T_rs;
+  const double P_rain = is_rain ? Pd : Pd * 0.0;
+  const double P_snow = is_rain ? Pd * 0.0 : Pd;
+  if (valid) {
+    d.P += Pd * p.da_m2 * dt;
+    d.Pmax = npmax(d.Pmax, Pd);
+    d.PR += P_rain * p.da_m2 * dt;
+    d.PS += P_snow * p.da_m2 * dt;
+  }
+  float e_sat_air;
+  if (!p.satterlund) {
+    e_sat_air = 6.11f * fexp(17.3f * T_air * frcp(T_air + 237.3f));
+  } else {
+    e_sat_air = fexp2((11.4f - 2353.0f * frcp(T_air + 273.15f)) * 3.3219280948873626f) * 0.01f;
+  }
+  const float e_air = Hum_sp * P_air * frcp(p.f_eps + p.f_one_minus_eps * Hum_sp) * 0.01f;
+  const float RH = e_air * frcp(e_sat_air);
+  const float log_term = flog(e_air * (1.0f / 6.1121f));
+  const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
+  const float T_surf = (h_snow > 0.0 || h_ice > 0.0) ? fminf(T_dew, 0.0f) : T_dew;
+  float e_sat_surf;
+  if (!p.satterlund) {
+    e_sat_surf = 6.11f * fexp(17.3f * T_surf * frcp(T_surf + 237.3f));
+  } else {
+    e_sat_surf = fexp2((11.4f - 2353.0f * frcp(T_surf + 273.15f)) * 3.3219280948873626f) * 0.01f;
+  }
+  const float dTs = T_air - T_surf;
+  float bot = (uz * uz) * T_K;
+  if (bot == 0.0f) bot = 0.01f;
+  const float Ri = p.f_gz * dTs * frcp(bot);
+  const float zr = (float)((p.z - h_snow) * p.inv_z0);
+  const float arg = p.f_kappa * frcp(flog(fmaxf(zr, 0.01f)));
+  const float Dn = uz * (arg * arg);
+  const float Dh = (Ri > 0.0f) ? Dn * frcp(1.0f + 10.0f * Ri) : Dn * (1.0f - 10.0f * Ri);
+  const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
+  const float W_p = 1.12f * fexp(0.0614f * T_dew);
+  const float e_surf = RH * e_sat_surf;
+  const float Qe = p.f_rho_air_Lv * Dh * (e_air - e_surf) * (p.f_lhc * frcp(p0));
+  // albedo with the exact fixed-point window
+  q_new = window_q(P_snow * dt * p.ws, p.qscale);
+  st.tot_q += (int64_t)q_new - (int64_t)q_old;
+  const float albedo = albedo_step<float>(p, st, st.tot_q >= p.thr_q, T_air);
+  // clear sky
+  const float m_opt = u.m_opt_f;
+  const float kf = u.k_et_flat_f;
+  const float tau = fminf(fmaxf(fexp((-0.1240f - 0.0207f * W_p) + (-0.0682f - 0.0248f * W_p) * m_opt) - p.f_dust, 0.0f), 1.0f);
+  // cos(omega*th + dlon) = cos(wth)cos(dlon) - sin(wth)sin(dlon)
+  const float cw = u.cos_wth_f * sf.cos_dlon - u.sin_wth_f * sf.sin_dlon;
+  float K_ET = u.isc_e0_f * ((u.cos_d_f * sf.cos_leq) * cw + sf.sin_leq * u.sin_d_f);
+  K_ET = fmaxf(K_ET, 0.0f);
+  const float gam_s = (1.0f - fexp((-0.0363f - 0.0084f * W_p) + (-0.0572f - 0.0173f * W_p) * m_opt)) + p.f_dust;
+  const float K_dif = 0.5f * gam_s * kf;
+  const float K_global = tau * kf + K_dif;
+  const float K_bs = 0.5f * gam_s * albedo * K_global;
+  float K_cs = tau * K_ET + K_dif + K_bs;
+  // dark mask: fp32 estimate, fp64 re-evaluation within 0.02 h of an edge
+  {
+    const float argf = fminf(fmaxf(-sf.tan_eq_f * u.tan_d_f, -1.0f), 1.0f);
+    const float acf = acosf(argf) * p.f_inv_omega;
+    const float th = u.th_f;
+    const float T_srf = fmaxf(sf.t_noon_f - acf, u.flat_sr_f);
+    const float T_ssf = fminf(sf.t_noon_f + acf, u.flat_ss_f);
+    const float m1 = th - T_srf, m2 = T_ssf - th;
+    bool dark;
+    if (fabsf(m1) < 0.02f || fabsf(m2) < 0.02f || !(m1 == m1) || !(m2 == m2)) {
+      dark = dark_exact(p, sf.tan_eq, sf.t_noon, up);
+    } else {
+      dark = (m1 <= 0.0f) || (m2 <= 0.0f);
+    }
+    if (dark) K_cs = 0.0f;
+  }
+  const float Qn_SW = K_cs * (1.0f - albedo);
+  float em_air;
+  if (!p.satterlund) {
+    const float x = e_air * 0.1f * frcp(T_K);
+    em_air = p.f_one_minus_F_172 * fexp2(flog2(x) * (1.0f / 7.0f)) * p.f_cloud_term + p.f_F;
+  } else {
+    em_air = 1.08f * (1.0f - fexp(-fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
+  }
+  const float T_surf_K = T_surf + 273.15f;
+  const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
+  const float LW_in = em_air * p.f_sigma * (ta2 * ta2);
+  const float LW_out = p.f_em_surf_sigma * (ts2 * ts2) + p.f_one_minus_em_surf * LW_in;
+  const float Qn_LW = LW_in - LW_out;
+  const float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
+  double T_wb = 0.0;
+  if (P_snow > 0.0) {
+    const float rh = RH;
+    const float twb = T_air * atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + atanf(T_air + rh) -
+                      atanf(rh - 1.676331f) +
+                      (0.00391838f * (rh * __builtin_sqrtf(rh))) * atanf(0.023101f * rh) - 4.86035f;
+    T_wb = (double)twb;
+  }
+  melt_and_mass<true>(p, (double)Q_sum, P_snow, P_rain, (double)RH, T_wb, st, o, d, valid);
+}
+
+}  // namespace tfg

@@ -1,0 +1,128 @@
+"""ctypes binding of the HIP engine library ``_tfg.so`` (C ABI: include/tfg.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).
+There is no CPU fallback: when the library is missing, or no GPU is visible,
+the engine raises instead of silently computing elsewhere.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import numpy as np
+
+__all__ = [
+    "LIB_PATH", "NativeError", "TfgParams", "UNIFORM_DTYPE", "lib", "load", "check",
+    "F32", "F64", "I32", "FIELD", "DIAG_NAMES",
+]
+
+LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
+
+F32, F64, I32 = 0, 1, 2
+OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_DOMAIN = 0, 1, 2, 3, 4
+
+# include/tfg.h field ids
+FIELD = {
+    "LW_in": 0, "P_air": 1, "Hum_sp": 2, "P": 3, "SW_in": 4, "T_air": 5, "uz": 6,
+    "h_snow": 7, "h_swe": 8, "SM": 9, "h_ice": 10, "h_iwe": 11, "IM": 12, "M_total": 13, "RH": 14,
+    "elev": 15, "slope": 16, "aspect": 17, "catch_id": 18,
+    "Eccs": 19, "Ecci": 20, "albedo": 21, "n": 22,
+}
+DIAG_NAMES = ["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"]
+
+
+class NativeError(RuntimeError):
+    """A nonzero status from the C ABI; the message is tfg_last_error()."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+class TfgParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        "dt", "da_m2", "lat", "lon", "sin_lat", "cos_lat",
+        "T_rain_snow", "dust_atten", "canopy_factor", "cloud_factor",
+        "rho_air", "rho_snow", "rho_ice", "rho_H2O", "h_active_layer", "T0",
+        "Cp_air", "Cp_ice", "Cp_snow", "g", "Lf", "eps", "kappa", "latent_heat_constant", "Lv",
+        "sigma", "sea_level_p0", "uni_gas_const", "M_mass_air", "z0_air", "em_surf",
+    )] + [("satterlund", ctypes.c_int32), ("ring_len", ctypes.c_int32)]
+
+
+# tfg_uniforms, one record per time step (numpy structured dtype, C layout)
+_U_D = ["th", "omega_th", "cos_wth", "sin_wth", "sin_d", "cos_d", "tan_d", "isc_e0", "m_opt",
+        "k_et_flat", "flat_sr", "flat_ss"]
+_U_F = ["th_f", "cos_wth_f", "sin_wth_f", "sin_d_f", "cos_d_f", "tan_d_f", "isc_e0_f", "m_opt_f",
+        "k_et_flat_f", "flat_sr_f", "flat_ss_f", "pad_f"]
+UNIFORM_DTYPE = np.dtype(
+    [(n, "<f8") for n in _U_D] + [(n, "<f4") for n in _U_F]
+    + [("frame", "<i4"), ("hist", "<i4"), ("slot", "<i4"), ("pad", "<i4")]
+)
+FLOAT_COPIES = list(zip(_U_F[:-1], ["th", "cos_wth", "sin_wth", "sin_d", "cos_d", "tan_d", "isc_e0", "m_opt", "k_et_flat", "flat_sr", "flat_ss"]))
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load and type the engine library (once).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"HIP engine library not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+            "There is no CPU fallback."
+        )
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, i64, i32, dp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
+    sigs = {
+        "tfg_abi_version": ([], i32),
+        "tfg_build_info": ([], ctypes.c_char_p),
+        "tfg_device_count": ([ctypes.POINTER(ctypes.c_int)], i32),
+        "tfg_create": ([ctypes.POINTER(TfgParams), i64, i64, i32, i32, i32, i32, i32, ctypes.POINTER(vp)], i32),
+        "tfg_destroy": ([vp], i32),
+        "tfg_set_stream": ([vp, vp], i32),
+        "tfg_get_stream": ([vp, ctypes.POINTER(vp)], i32),
+        "tfg_set_field": ([vp, i32, i32, vp, i32, i64, i32], i32),
+        "tfg_get_field": ([vp, i32, i32, vp, i32, i64, i32], i32),
+        "tfg_init_state": ([vp], i32),
+        "tfg_step": ([vp, vp, i64], i32),
+        "tfg_set_fuse": ([vp, i32], i32),
+        "tfg_get_diag": ([vp, dp, i32], i32),
+        "tfg_reset_diag": ([vp], i32),
+        "tfg_sync": ([vp], i32),
+        "tfg_fill_synthetic": ([vp, ctypes.c_uint64, i64, i64, ctypes.POINTER(ctypes.c_float), i32], i32),
+        "tfg_last_error": ([vp], ctypes.c_char_p),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    if L.tfg_abi_version() != 1:
+        raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != 1")
+    _lib = L
+    return L
+
+
+def lib() -> ctypes.CDLL:
+    return load()
+
+
+def check(rc: int, handle=None) -> None:
+    if rc != OK:
+        msg = lib().tfg_last_error(handle)
+        raise NativeError(rc, (msg or b"").decode() or f"tfg error {rc}")
+
+
+def exported_symbols() -> list[str]:
+    """Names declared in include/tfg.h that the loaded library exports."""
+    L = load()
+    return [n for n in (
+        "tfg_abi_version", "tfg_build_info", "tfg_device_count", "tfg_create", "tfg_destroy",
+        "tfg_set_stream", "tfg_get_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
+        "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
+        "tfg_fill_synthetic", "tfg_last_error",
+    ) if hasattr(L, n)]

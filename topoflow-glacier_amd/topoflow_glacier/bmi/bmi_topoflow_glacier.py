@@ -1,0 +1,395 @@
+"""BmiTopoflowGlacier -- the reference's BMI surface on the MI355X engine.
+
+Drop-in for src/topoflow_glacier/bmi/bmi_topoflow_glacier.py: same class name,
+variable names, units, order and float64 host arrays; same YAML loader
+(config.py); same error types.  What changes is where ``update()`` runs: the
+46 NumPy calls of :413-465 become one launch of the fused HIP kernel over all
+cells of the grid (C ABI include/tfg.h via ctypes).
+
+Modes
+  * single catchment (the reference's case, ny = nx = 1): fp64 engine with the
+    reference's operation order; inputs/outputs mirrored eagerly, so
+    ``get_value_ptr`` references stay live exactly as in the reference.
+  * grid (``ny``/``nx`` in the YAML): fp32 engine by default; BMI arrays have
+    ny*nx float64 entries, refreshed from the device when read.
+
+Additive fixes (the reference versions are broken):
+``get_current_time``/``get_time_step``/``get_time_units``/``get_end_time``,
+``update_until`` (fused multi-step launch), ``get_var_units``,
+``get_value_at_indices``, the grid-description functions.
+"""
+
+from __future__ import annotations
+
+from datetime import timedelta
+from pathlib import Path
+
+import numpy as np
+import yaml
+
+from .. import _native as nat
+from ..engine import GlacierEngine
+from ..physics.clock import parse_time
+from ..physics.context import Context, build_context
+from .bmi_base import BmiBase
+from .config import TopoflowGlacierConfig
+from .logger import configure_logging, logger
+
+__all__ = ["BmiTopoflowGlacier"]
+
+# bmi_topoflow_glacier.py:18-37 (names, units, order)
+_dynamic_input_vars = [
+    ("land_surface_radiation~incoming~longwave__energy_flux", "W m-2"),
+    ("land_surface_air__pressure", "Pa"),
+    ("atmosphere_air_water~vapor__relative_saturation", "kg kg-1"),
+    ("atmosphere_water__liquid_equivalent_precipitation_rate", "mm h-1"),
+    ("land_surface_radiation~incoming~shortwave__energy_flux", "W m-2"),
+    ("land_surface_air__temperature", "degC"),
+    ("wind_speed_UV", "m sec-1"),
+]
+_output_vars = [
+    ("snowpack__depth", "m"),
+    ("snowpack__liquid-equivalent_depth", "m"),
+    ("snowpack__melt_volume_flux", "m s-1"),
+    ("glacier_ice__thickness", "m"),
+    ("glacier__liquid_equivalent_depth", "m"),
+    ("glacier_ice__melt_volume_flux", "m s-1"),
+    ("land_surface_water__runoff_volume_flux", "m s-1"),
+    ("atmosphere_bottom_air_water-vapor__relative_saturation", "-"),
+]
+INTERNAL_NAME_CROSSWALK = {
+    "land_surface_radiation~incoming~longwave__energy_flux": "LW_in",
+    "land_surface_air__pressure": "P_air",
+    "atmosphere_air_water~vapor__relative_saturation": "Hum_sp",
+    "atmosphere_water__liquid_equivalent_precipitation_rate": "P",
+    "land_surface_radiation~incoming~shortwave__energy_flux": "SW_in",
+    "land_surface_air__temperature": "T_air",
+    "wind_speed_UV": "uz",
+    "snowpack__depth": "h_snow",
+    "snowpack__liquid-equivalent_depth": "h_swe",
+    "snowpack__melt_volume_flux": "SM",
+    "glacier_ice__thickness": "h_ice",
+    "glacier__liquid_equivalent_depth": "h_iwe",
+    "glacier_ice__melt_volume_flux": "IM",
+    "land_surface_water__runoff_volume_flux": "M_total",
+    "atmosphere_bottom_air_water-vapor__relative_saturation": "RH",
+}
+EXTERNAL_NAME_CROSSWALK = {v: k for k, v in INTERNAL_NAME_CROSSWALK.items()}
+_PHYSICS_INPUTS = ("P", "T_air", "Hum_sp", "P_air", "uz")  # LW_in / SW_in are never read (:1122, :1235)
+_EAGER_MAX_CELLS = 4096
+
+
+def crosswalk_to_external(name: str) -> str:
+    return INTERNAL_NAME_CROSSWALK[name]
+
+
+def crosswalk_to_interal(name: str) -> str:  # reference spelling (:98)
+    return EXTERNAL_NAME_CROSSWALK[name]
+
+
+def first_containing(name: str, *states: Context) -> Context:
+    """First context holding `name`, else KeyError (:1896-1901)."""
+    for s in states:
+        if name in s:
+            return s
+    raise KeyError(f"unknown name: {name!s}")
+
+
+def _accessor(external: str, ctx: str):
+    def getter(self):
+        return self._mirror(external)
+
+    def setter(self, value):
+        self.set_value(external, value)
+
+    return property(getter, setter, doc=f"BMI variable {external}")
+
+
+class BmiTopoflowGlacier(BmiBase):
+    """BMI composition wrapper for TopoflowGlacier on MI355X."""
+
+    def __init__(self) -> None:
+        self._dynamic_inputs = build_context(_dynamic_input_vars)
+        self._outputs = build_context(_output_vars)
+        self._timestep: int = 0
+        self._engine: GlacierEngine | None = None
+        self._stale: set[str] = set()
+        self._beta_invalid = False
+        configure_logging()
+
+    # reference properties (:124-272)
+    P = _accessor("atmosphere_water__liquid_equivalent_precipitation_rate", "in")
+    T_air = _accessor("land_surface_air__temperature", "in")
+    LW_in = _accessor("land_surface_radiation~incoming~longwave__energy_flux", "in")
+    SW_in = _accessor("land_surface_radiation~incoming~shortwave__energy_flux", "in")
+    P_air = _accessor("land_surface_air__pressure", "in")
+    Hum_sp = _accessor("atmosphere_air_water~vapor__relative_saturation", "in")
+    uz = _accessor("wind_speed_UV", "in")
+    SM = _accessor("snowpack__melt_volume_flux", "out")
+    IM = _accessor("glacier_ice__melt_volume_flux", "out")
+    h_swe = _accessor("snowpack__liquid-equivalent_depth", "out")
+    h_iwe = _accessor("glacier__liquid_equivalent_depth", "out")
+    h_snow = _accessor("snowpack__depth", "out")
+    h_ice = _accessor("glacier_ice__thickness", "out")
+    M_total = _accessor("land_surface_water__runoff_volume_flux", "out")
+    RH = _accessor("atmosphere_bottom_air_water-vapor__relative_saturation", "out")
+
+    # ------------------------------------------------------------------ setup
+    def initialize(self, config_file: str | Path) -> None:
+        """Read the YAML config and set up state (reference :274-411)."""
+        with open(config_file) as f:
+            config = yaml.safe_load(f)
+        self.cfg = TopoflowGlacierConfig.model_validate(config)
+        cfg = self.cfg
+        self.hours_per_day = np.float64(24)
+        self.seconds_per_Day = np.float64(24) * 3600
+        self.sec_per_year = np.float64(3600) * 24 * 365
+        self.mps_to_mmph = np.float64(3600000)
+        self.mmph_to_mps = np.float64(1) / np.float64(3600000)
+        self.dt = cfg.dt
+        self.days_per_dt = self.dt / 86400
+        self.C_to_K = 273.15
+        self.K_to_C = -273.15
+        self.twopi = np.float64(2) * np.pi
+        self.one_seventh = np.float64(1) / 7
+        self.da_km2 = cfg.da
+        self.da_m2 = self.da_km2 * 1e6
+        self.slopes = cfg.slope
+        self.ws_density_ratio = np.float64(cfg.rho_H2O) / np.float64(cfg.rho_snow)
+        self.wi_density_ratio = np.float64(cfg.rho_H2O) / np.float64(cfg.rho_ice)
+        self.ny, self.nx = cfg.ny, cfg.nx
+        n = self.ny * self.nx
+        self.n_cells = n
+        self._dynamic_inputs = build_context(_dynamic_input_vars, n)
+        self._outputs = build_context(_output_vars, n)
+        self._eager = n <= _EAGER_MAX_CELLS
+        engine = cfg.engine or ("float64" if n == 1 else "float32")
+        self._engine = GlacierEngine(cfg, self.ny, self.nx, engine=engine, device=cfg.device,
+                                     fuse_steps=cfg.fuse_steps)
+        eng = self._engine
+        eng.set_field("elev", np.float64(cfg.elev))
+        try:
+            eng.set_field("slope", np.float64(cfg.slope))
+            self._beta_invalid = False
+        except nat.NativeError as e:
+            if e.code != nat.ERR_DOMAIN:
+                raise
+            # reference: logs and leaves beta unset; the first update() then fails (:1106-1111)
+            logger.error("ERROR: In met_base.py, some slope angles are out of range.  Returning without setting beta.")
+            self._beta_invalid = True
+        eng.set_field("aspect", np.float64(cfg.aspect))
+        for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
+            v = np.float64(getattr(cfg, key))
+            self._outputs.set_value(crosswalk_to_external(name), v)
+            eng.set_field(name, v)
+        eng.init_state()
+        self._stale.clear()
+        self._dirty_outputs: set[str] = set()
+        self._timestep = 0
+        start = parse_time(cfg.start_time)
+        self.start_year, self.start_month, self.start_day, self.start_hour = start.year, start.month, start.day, start.hour
+        end = parse_time(cfg.end_time)
+        self.end_year, self.end_month, self.end_day, self.end_hour = end.year, end.month, end.day, end.hour
+        self.start_time = start
+        self.start_datetime = start  # advanced each step, as in the reference (:1866-1893)
+        self.year = start.year
+        self.julian_day = None
+        self.TSN_offset = None
+        self.GMT_offset = None
+
+    # ----------------------------------------------------------------- update
+    def _require(self) -> GlacierEngine:
+        if self._engine is None:
+            raise RuntimeError("initialize() has not been called")
+        if self._beta_invalid:
+            raise AttributeError("'BmiTopoflowGlacier' object has no attribute 'beta'")
+        return self._engine
+
+    def _push_inputs(self) -> None:
+        eng = self._engine
+        for name in _PHYSICS_INPUTS:
+            eng.set_field(name, self._dynamic_inputs.value(crosswalk_to_external(name)))
+        for name in sorted(self._dirty_outputs):
+            eng.set_field(name, self._outputs.value(crosswalk_to_external(name)))
+        self._dirty_outputs.clear()
+
+    def _after_steps(self, nsteps: int) -> None:
+        k = self._timestep + nsteps - 1
+        jd, yr, gmt, tsn = self._engine.clock.calendar(k, 1)
+        self.julian_day, self.year, self.GMT_offset, self.TSN_offset = float(jd[0]), int(yr[0]), float(gmt[0]), float(tsn[0])
+        self.start_datetime = self.start_time + timedelta(hours=self.dt * (k + 1))
+        self._timestep += nsteps
+        self._stale = {crosswalk_to_internal_out(n) for n, _ in _output_vars}
+        if self._eager:
+            for name in list(self._stale):
+                self._refresh(name)
+
+    def update(self) -> None:
+        """Advance one time step (reference :413-465) on the GPU."""
+        eng = self._require()
+        self._push_inputs()
+        eng.run(1)
+        self._after_steps(1)
+
+    def update_until(self, time: float) -> None:
+        """Advance to `time` [s] with one fused multi-step run (reference :471-490)."""
+        if time <= self.get_current_time():
+            logger.warning(f"no update performed: {time=} <= current_time={self.get_current_time()}")
+            return None
+        n_steps, remainder = divmod(time - self.get_current_time(), self.get_time_step())
+        if remainder != 0:
+            logger.warning(f"time is not multiple of time step size. updating until: {time - remainder=} ")
+        n_steps = int(n_steps)
+        if n_steps <= 0:
+            return None
+        eng = self._require()
+        self._push_inputs()
+        eng.run(n_steps)
+        self._after_steps(n_steps)
+
+    def finalize(self) -> None:
+        """Release the device shard (reference :467-469)."""
+        if self._engine is not None:
+            for name in list(self._stale):
+                self._refresh(name)
+            self._engine.close()
+            self._engine = None
+
+    # ------------------------------------------------------------- mirrors
+    def _refresh(self, internal: str) -> None:
+        ext = crosswalk_to_external(internal)
+        self._outputs.value(ext)[:] = self._engine.get_field(internal)
+        self._stale.discard(internal)
+
+    def _mirror(self, external: str) -> np.ndarray:
+        ctx = first_containing(external, self._outputs, self._dynamic_inputs)
+        if ctx is self._outputs and self._engine is not None:
+            internal = crosswalk_to_interal(external)
+            if internal in self._stale:
+                self._refresh(internal)
+        return ctx.value(external)
+
+    # ------------------------------------------------------------ BMI vars
+    def get_component_name(self) -> str:
+        return "Topoflow-Glacier"
+
+    def get_input_item_count(self) -> int:
+        return len(self._dynamic_inputs)
+
+    def get_output_item_count(self) -> int:
+        return len(self._outputs)
+
+    def get_input_var_names(self) -> tuple[str, ...]:
+        return tuple(self._dynamic_inputs.names())
+
+    def get_output_var_names(self) -> tuple[str, ...]:
+        return tuple(self._outputs.names())
+
+    def set_value(self, name: str, src) -> None:
+        ctx = first_containing(name, self._outputs, self._dynamic_inputs)
+        ctx.set_value(name, src)
+        if ctx is self._outputs:
+            internal = crosswalk_to_interal(name)
+            self._stale.discard(internal)
+            self._dirty_outputs.add(internal)
+
+    def set_value_at_indices(self, name: str, inds, src) -> None:
+        self._mirror(name)  # refresh first so the untouched entries stay current
+        ctx = first_containing(name, self._outputs, self._dynamic_inputs)
+        ctx.set_value_at_indices(name, np.asarray(inds), np.asarray(src))
+        if ctx is self._outputs:
+            self._dirty_outputs.add(crosswalk_to_interal(name))
+
+    def get_value(self, name: str, dest):
+        """Copy of a variable, flattened into `dest` (reference :1810-1824)."""
+        value = self.get_value_ptr(name)
+        try:
+            dest[:] = value.flatten()
+        except Exception as e:
+            raise RuntimeError(f"Could not return value {name} as flattened array") from e
+        return dest
+
+    def get_value_ptr(self, name: str):
+        return self._mirror(name)
+
+    def get_value_at_indices(self, name: str, dest, inds):
+        self._mirror(name)
+        return first_containing(name, self._outputs, self._dynamic_inputs).value_at_indices(name, dest, np.asarray(inds))
+
+    def get_var_itemsize(self, name: str) -> int:
+        return self.get_value_ptr(name).itemsize
+
+    def get_var_nbytes(self, name: str) -> int:
+        return self.get_value_ptr(name).nbytes
+
+    def get_var_type(self, name: str) -> str:
+        return str(self.get_value_ptr(name).dtype)
+
+    def get_var_units(self, name: str) -> str:
+        return first_containing(name, self._outputs, self._dynamic_inputs).unit(name)
+
+    def get_var_grid(self, name: str) -> int:
+        first_containing(name, self._outputs, self._dynamic_inputs)
+        return 0
+
+    def get_var_location(self, name: str) -> str:
+        first_containing(name, self._outputs, self._dynamic_inputs)
+        return "node"
+
+    # ------------------------------------------------------------------ grid
+    def get_grid_rank(self, grid: int) -> int:
+        return 2
+
+    def get_grid_size(self, grid: int) -> int:
+        return int(getattr(self, "n_cells", 1))
+
+    def get_grid_shape(self, grid: int, shape):
+        shape[:] = (self.ny, self.nx)
+        return shape
+
+    def get_grid_spacing(self, grid: int, spacing):
+        d = float(np.sqrt(self.cfg.da) * 1000.0)
+        spacing[:] = (d, d)
+        return spacing
+
+    def get_grid_origin(self, grid: int, origin):
+        origin[:] = (0.0, 0.0)
+        return origin
+
+    def get_grid_type(self, grid: int) -> str:
+        return "uniform_rectilinear"
+
+    # ------------------------------------------------------------------ time
+    def get_start_time(self) -> float:
+        return 0.0
+
+    def get_time_step(self) -> float:
+        return float(self.dt) * 3600.0
+
+    def get_time_units(self) -> str:
+        return "s"
+
+    def get_current_time(self) -> float:
+        return self._timestep * self.get_time_step()
+
+    def get_end_time(self) -> float:
+        return (parse_time(self.cfg.end_time) - parse_time(self.cfg.start_time)).total_seconds()
+
+    # ------------------------------------------------- diagnostics / state
+    def _diag(self, i: int) -> np.ndarray:
+        return np.array([self._engine.diagnostics()[:, i].sum() if i < 5 else self._engine.diagnostics()[:, i].max()])
+
+    vol_P = property(lambda self: self._diag(0), doc="sum(P*da*dt) (:558-568)")
+    vol_PR = property(lambda self: self._diag(1), doc="sum(P_rain*da*dt) (:606-614)")
+    vol_PS = property(lambda self: self._diag(2), doc="sum(P_snow*da*dt) (:616-624)")
+    vol_SM = property(lambda self: self._diag(3), doc="sum(SM*da*dt*3600) (:1482-1487)")
+    vol_IM = property(lambda self: self._diag(4), doc="sum(IM*da*dt*3600) (:1489-1494)")
+    P_max = property(lambda self: self._diag(5), doc="max P (:570-576)")
+    Eccs = property(lambda self: self._engine.get_field("Eccs"), doc="snowpack cold content [J m-2]")
+    Ecci = property(lambda self: self._engine.get_field("Ecci"), doc="ice cold content [J m-2]")
+    albedo = property(lambda self: self._engine.get_field("albedo"), doc="surface albedo")
+    n = property(lambda self: self._engine.get_field("n"), doc="days since last major snowfall")
+
+
+def crosswalk_to_internal_out(external: str) -> str:
+    return EXTERNAL_NAME_CROSSWALK[external]

@@ -1,0 +1,116 @@
+"""YAML configuration schema (drop-in for config.py:6-115 of the reference).
+
+Every key the reference accepts is accepted here with the same default and the
+same validation, so reference YAML files (config/*.yaml) load unchanged.  Two
+deliberate, additive differences:
+
+* ``dt`` also accepts a float (the reference types it ``int`` hours,
+  config.py:15, which rules out the 15-minute step of BASELINE config 5);
+  integer values keep their int type, so arithmetic is unchanged.
+* ``start_time`` / ``end_time`` written as bare YAML integers
+  (config/cat-3062784.yaml, cat-3062924.yaml, cat-3062927.yaml) are accepted
+  as their digit strings; the reference's loader rejects those files.
+* grid / engine keys the reference does not have (all optional):
+  ``ny``, ``nx`` (grid shape, default 1 x 1 = the reference's single
+  catchment), ``engine`` ("float64" | "float32"; default float64 for one cell,
+  float32 for grids), ``device`` (HIP device ordinal, default LOCAL_RANK or 0),
+  ``time_zone`` (IANA name; default looked up from lat/lon),
+  ``fuse_steps`` (time steps fused per kernel launch, default 24).
+
+Unknown keys are ignored, as in the reference (pydantic default).
+"""
+
+from __future__ import annotations
+
+from typing import Literal
+
+from pydantic import BaseModel, ConfigDict, Field, field_validator
+
+__all__ = ["TopoflowGlacierConfig"]
+
+
+class TopoflowGlacierConfig(BaseModel):
+    """Validated model configuration."""
+
+    model_config = ConfigDict(arbitrary_types_allowed=True)
+
+    # --- required (config.py:13-27) ---------------------------------------
+    site_prefix: str
+    forcing_file: str
+    dt: int | float = Field(ge=0, description="time step [hours]")
+    start_time: str
+    end_time: str
+    da: float = Field(description="area [km2] (per cell for grids)")
+    slope: float
+    lat: float
+    lon: float
+    h0_snow: float
+    h0_ice: float
+    h0_swe: float
+    h0_iwe: float
+    elev: float
+    # --- defaulted parameters (config.py:28-33) ----------------------------
+    T_rain_snow: float = 1.0
+    aspect: float = 0.0
+    dust_atten: float = Field(0.08, ge=0.0, le=0.2)
+    canopy_factor: float = Field(0.0, ge=0.0, le=1.0)
+    cloud_factor: float = Field(0.0, ge=0.0, le=1.0)
+    # --- physical constants (config.py:38-62) ------------------------------
+    rho_air: float = 1.2614
+    rho_snow: float = 50.0
+    rho_ice: float = 917.0
+    rho_H2O: float = 1000.0
+    h_active_layer: float = 0.125
+    T0: float = -0.2
+    Cp_air: float = 1005.7
+    Cp_ice: float = 2060.0
+    Cp_snow: float = 2090.0
+    g: float = 9.81
+    Lf: float = 334000.0
+    eps: float = 0.622
+    kappa: float = 0.408
+    latent_heat_constant: float = 0.622
+    Lv: float = 2500000
+    sigma: float = 5.67 * 10 ** (-8)
+    sea_level_p0: float = 101325.0
+    sea_level_T0: float = 288.15
+    T_lapse_rate: float = 0.0065
+    uni_gas_const: float = 8.3144598
+    M_mass_air: float = 0.0289644
+    # --- glacier-dynamics fields (config.py:64-85): accepted, unused --------
+    min_glacier_thick: float = 1.0
+    glens_A: float = 2.142e-16
+    B: float = 0.0012
+    char_sliding_vel: float = 10.0
+    char_tau_bed: float = 100000.0
+    depth_to_water_table: float = 20.0
+    max_float_fraction: float = 80.0
+    Hp_eff: float = 20.0
+    init_ELA: float = 3350.0
+    ELA_step_size: float = -10.0
+    ELA_step_interval: float = 500.0
+    grad_Bz: float = 0.01
+    max_Bz: float = 2.0
+    spinup_time: float = 200.0
+    sea_level: float = -100.0
+    z0_air: float = Field(0.01, ge=0.0001, le=0.1)
+    em_surf: float = Field(0.985, ge=0.9, le=1)
+    geothermal_heat_flux: float = 1575000.0
+    geothermal_gradient: float = -0.0255
+    # --- legacy toggles (config.py:94-101) ---------------------------------
+    PRECIP_ONLY: bool = False
+    P_factor: float = 1.0
+    SATTERLUND: bool = False
+
+    # --- additive keys of this build ---------------------------------------
+    ny: int = Field(1, ge=1)
+    nx: int = Field(1, ge=1)
+    engine: Literal["float64", "float32"] | None = None
+    device: int | None = None
+    time_zone: str | None = None
+    fuse_steps: int = Field(24, ge=1)
+
+    @field_validator("start_time", "end_time", mode="before")
+    @classmethod
+    def _digits_as_text(cls, v):
+        return str(v) if isinstance(v, int) and not isinstance(v, bool) else v

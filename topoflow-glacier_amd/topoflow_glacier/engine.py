@@ -1,0 +1,176 @@
+"""GlacierEngine: one grid shard of the HIP energy-balance engine.
+
+Thin Python owner of a ``tfg_handle`` (include/tfg.h).  It converts a
+validated configuration into ``tfg_params``, moves rasters in and out, and
+advances the model with :meth:`run`, which hands a block of per-step uniforms
+(:class:`~topoflow_glacier.physics.clock.StepClock`) to ``tfg_step``; the
+library fuses up to ``fuse_steps`` steps per kernel launch.
+
+All arithmetic happens in the HIP kernels; this class never computes physics.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _native as nat
+from .physics.clock import StepClock
+
+__all__ = ["GlacierEngine", "params_from_config"]
+
+_ENGINES = {"float32": nat.F32, "float64": nat.F64}
+_NP = {nat.F32: np.float32, nat.F64: np.float64}
+
+
+def params_from_config(cfg) -> nat.TfgParams:
+    """tfg_params from a TopoflowGlacierConfig (or any object with its fields)."""
+    p = nat.TfgParams()
+    for name, _ in nat.TfgParams._fields_:
+        if name in ("da_m2", "sin_lat", "cos_lat", "satterlund", "ring_len"):
+            continue
+        setattr(p, name, float(getattr(cfg, name)))
+    p.da_m2 = float(cfg.da) * 1e6  # :293-294
+    lat_rad = cfg.lat * (np.pi / np.float64(180))  # as Equivalent_Latitude computes it
+    p.sin_lat = float(np.sin(lat_rad))
+    p.cos_lat = float(np.cos(lat_rad))
+    p.satterlund = int(bool(cfg.SATTERLUND))
+    p.ring_len = int(3 * np.float64(24) / cfg.dt)  # :296
+    return p
+
+
+class GlacierEngine:
+    """A ny x nx shard resident on one GPU."""
+
+    def __init__(self, cfg, ny: int, nx: int, engine: str = "float32", device: int | None = None,
+                 n_frames: int = 1, hist_depth: int = 1, n_catch: int = 1, fuse_steps: int | None = None,
+                 row0: int = 0):
+        self.lib = nat.load()
+        self.cfg = cfg
+        self.ny, self.nx, self.n = int(ny), int(nx), int(ny) * int(nx)
+        self.row0 = int(row0)
+        self.engine = engine
+        self.dtype_code = _ENGINES[engine]
+        self.np_dtype = _NP[self.dtype_code]
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", 0))
+        self.device = int(device)
+        self.n_frames, self.hist_depth, self.n_catch = int(n_frames), int(hist_depth), int(n_catch)
+        self.params = params_from_config(cfg)
+        self.ring_len = int(self.params.ring_len)
+        h = ctypes.c_void_p()
+        nat.check(self.lib.tfg_create(ctypes.byref(self.params), self.ny, self.nx, self.dtype_code, self.device,
+                                      self.n_frames, self.hist_depth, self.n_catch, ctypes.byref(h)))
+        self.h = h
+        self.fuse_steps = int(fuse_steps or getattr(cfg, "fuse_steps", 24) or 24)
+        nat.check(self.lib.tfg_set_fuse(self.h, self.fuse_steps), self.h)
+        self.clock = StepClock(cfg.start_time, cfg.dt, cfg.lat, cfg.lon, getattr(cfg, "time_zone", None),
+                               ring_len=self.ring_len)
+        self.step_index = 0  # model steps completed
+
+    # -- lifetime -------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "h", None) is not None and self.h.value:
+            self.lib.tfg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int) -> None:
+        nat.check(rc, self.h)
+
+    # -- fields -----------------------------------------------------------------
+    def set_field(self, name: str, values, index: int = 0) -> None:
+        """Copy a host array (broadcast to n cells) or a torch CUDA tensor into a field."""
+        fid = nat.FIELD[name]
+        if hasattr(values, "data_ptr") and getattr(values, "is_cuda", False):
+            t = values.contiguous()
+            code = {4: nat.F32, 8: nat.F64}[t.element_size()] if name != "catch_id" else nat.I32
+            if t.numel() != self.n:
+                raise ValueError(f"{name}: {t.numel()} values for {self.n} cells")
+            self._chk(self.lib.tfg_set_field(self.h, fid, index, ctypes.c_void_p(t.data_ptr()), code, self.n, 1))
+            return
+        if name == "catch_id":
+            a = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.int32), (self.n,)))
+            code = nat.I32
+        else:
+            a = np.asarray(values)
+            a = np.ascontiguousarray(np.broadcast_to(a.astype(np.float32 if a.dtype == np.float32 else np.float64), (self.n,)))
+            code = nat.F32 if a.dtype == np.float32 else nat.F64
+        self._chk(self.lib.tfg_set_field(self.h, fid, index, a.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
+
+    def get_field(self, name: str, index: int | None = None, dtype=np.float64) -> np.ndarray:
+        """Host copy of a field.  Outputs default to the newest history slot."""
+        fid = nat.FIELD[name]
+        if index is None:
+            index = self.last_hist if name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") else 0
+        if name == "catch_id":
+            out = np.empty(self.n, dtype=np.int32)
+            code = nat.I32
+        else:
+            out = np.empty(self.n, dtype=dtype)
+            code = nat.F32 if out.dtype == np.float32 else nat.F64
+        self._chk(self.lib.tfg_get_field(self.h, fid, index, out.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
+        return out
+
+    @property
+    def last_hist(self) -> int:
+        return (self.step_index - 1) % self.hist_depth if self.step_index > 0 else 0
+
+    def init_state(self) -> None:
+        """initialize()-time state from the depth rasters (reference :389-395)."""
+        self._chk(self.lib.tfg_init_state(self.h))
+        self.step_index = 0
+
+    def fill_synthetic(self, seed: int, diurnal: np.ndarray, nx_global: int | None = None) -> None:
+        d = np.ascontiguousarray(diurnal, dtype=np.float32)
+        self._chk(self.lib.tfg_fill_synthetic(self.h, int(seed), self.row0, int(nx_global or self.nx),
+                                              d.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), self.n_frames))
+        self.step_index = 0
+
+    # -- time stepping ------------------------------------------------------------
+    def uniforms(self, nsteps: int, frames=None) -> np.ndarray:
+        k0 = self.step_index
+        hist = (np.arange(k0, k0 + nsteps) % self.hist_depth).astype(np.int32)
+        if frames is None:
+            frames = (np.arange(k0, k0 + nsteps) % self.n_frames).astype(np.int32)
+        return self.clock.uniforms(k0, nsteps, frames=frames, hist=hist)
+
+    def run(self, nsteps: int = 1, uniforms: np.ndarray | None = None, frames=None) -> None:
+        """Advance nsteps model steps (update() / update_until(), :413-490).
+        Asynchronous: returns once the launches are queued."""
+        if nsteps <= 0:
+            return
+        u = self.uniforms(nsteps, frames) if uniforms is None else uniforms
+        u = np.ascontiguousarray(u, dtype=nat.UNIFORM_DTYPE)
+        if len(u) != nsteps:
+            raise ValueError("one uniform record per step")
+        self._chk(self.lib.tfg_step(self.h, u.ctypes.data_as(ctypes.c_void_p), nsteps))
+        self.step_index += nsteps
+
+    def sync(self) -> None:
+        self._chk(self.lib.tfg_sync(self.h))
+
+    def set_stream(self, stream_ptr: int | None) -> None:
+        self._chk(self.lib.tfg_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)))
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        self._chk(self.lib.tfg_get_stream(self.h, ctypes.byref(s)))
+        return s.value or 0
+
+    # -- mass balance -------------------------------------------------------------
+    def diagnostics(self) -> np.ndarray:
+        """[n_catch][6] = vol_P, vol_PR, vol_PS, vol_SM, vol_IM, P_max of this shard."""
+        out = np.zeros((self.n_catch, 6), dtype=np.float64)
+        self._chk(self.lib.tfg_get_diag(self.h, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), self.n_catch))
+        return out
+
+    def reset_diagnostics(self) -> None:
+        self._chk(self.lib.tfg_reset_diag(self.h))

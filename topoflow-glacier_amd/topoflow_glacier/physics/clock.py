@@ -1,0 +1,173 @@
+"""Model clock and the per-step uniform scalars of the hot path.
+
+For a grid with one latitude/longitude (the reference's catchment centroid,
+config.py:21-22) everything in ``update_julian_day`` (bmi_topoflow_glacier.py
+:957-1004) and the latitude-only part of ``Clear_Sky_Radiation``
+(solar_funcs.py:894-953) is the same for every cell.  ``StepClock`` evaluates
+it on the host once per step, in float64 numpy with the reference's operation
+order (so the fp64 engine sees bit-identical values), vectorised over a block
+of steps, and packs it into ``tfg_uniforms`` records for the kernel.
+
+Time convention (reference :1866-1893): the model datetime is advanced by
+``dt`` hours *before* it is used, so step k (0-based) uses start + (k+1)*dt.
+The UTC offset is DST-aware (zoneinfo, SF:1616-1637); the IANA zone comes from
+``cfg.time_zone`` or from :func:`zone_for` (timezonefinder is not available
+offline).
+"""
+
+from __future__ import annotations
+
+from datetime import datetime, timedelta
+from functools import lru_cache
+from zoneinfo import ZoneInfo
+
+import numpy as np
+
+from .._native import FLOAT_COPIES, UNIFORM_DTYPE
+
+__all__ = ["StepClock", "zone_for", "parse_time", "PERIHELION"]
+
+_RAD = np.pi / np.float64(180)
+_OMEGA = (np.float64(360) / np.float64(24)) * (np.pi / np.float64(180))  # SF:257-258
+
+# Day-of-January and hour of Earth's perihelion, 1981-2060 (SF:1167-1248).
+_TP = (
+    "2:2 4:11 2:15 3:22 3:20 2:5 4:23 3:0 1:22 4:17 3:3 3:15 4:3 2:6 4:11 4:7 2:0 4:21 3:13 3:5 "
+    "4:9 2:14 4:5 4:18 2:1 4:15 3:20 3:0 4:15 3:0 3:19 5:0 2:5 4:12 4:7 2:23 4:14 3:6 3:5 5:8 "
+    "2:14 4:7 4:16 3:1 4:13 3:17 3:3 5:12 2:18 3:10 4:21 3:5 4:12 4:5 3:1 5:14 3:4 3:5 5:7 3:12 "
+    "3:22 4:9 2:22 5:13 3:15 3:1 5:12 3:18 3:10 4:20 3:6 5:9 3:22 2:18 5:12 4:4 3:3 5:4 3:11 4:23"
+)
+PERIHELION = {1981 + i: tuple(int(x) for x in v.split(":")) for i, v in enumerate(_TP.split())}
+
+# Coarse IANA zones for the NextGen / NWM domain (first match wins).  The
+# reference resolves the zone with timezonefinder polygons; every reference
+# config and test lies in America/Los_Angeles.
+_ZONES = [
+    ((51.0, 72.0, -170.0, -129.0), "America/Anchorage"),
+    ((18.5, 23.0, -161.0, -154.0), "Pacific/Honolulu"),
+    ((32.0, 49.5, -125.0, -114.0), "America/Los_Angeles"),
+    ((31.0, 49.5, -114.0, -102.0), "America/Denver"),
+    ((25.0, 49.5, -102.0, -87.0), "America/Chicago"),
+    ((24.0, 49.5, -87.0, -66.0), "America/New_York"),
+]
+
+
+def zone_for(lat: float, lon: float) -> str:
+    """IANA time zone for a point in the supported domain (else ValueError,
+    as the reference raises when no zone is found, SF:1629-1630)."""
+    for (la0, la1, lo0, lo1), name in _ZONES:
+        if la0 <= lat <= la1 and lo0 <= lon <= lo1:
+            return name
+    raise ValueError(f"Could not determine timezone for lat={lat}, lon={lon}; set `time_zone` in the config.")
+
+
+def parse_time(s) -> datetime:
+    """'YYYYMMDDHH' or 'YYYYMMDD-HH' (reference :512-517)."""
+    s = str(s).strip()
+    return datetime.strptime(s, "%Y%m%d-%H" if "-" in s else "%Y%m%d%H")
+
+
+def _julian_day_of_january(day: int, hour: int) -> np.float64:
+    # Julian_Day(1, day, hour) with year=None (SF:958-1009)
+    return np.float64(0) + np.maximum(day - 1, 0) + (hour / np.float64(24))
+
+
+@lru_cache(maxsize=None)
+def _perihelion_jd(year: int) -> np.float64:
+    if year not in PERIHELION:
+        # the reference silently substitutes the wall-clock year (SF:1158-1162);
+        # that makes results depend on when they are run, so refuse instead.
+        raise ValueError(f"Earth perihelion table covers 1981-2060, got year {year}")
+    d, h = PERIHELION[year]
+    return _julian_day_of_january(d, h)
+
+
+def _equation_of_time_hours(JD: np.ndarray, years: np.ndarray) -> np.ndarray:
+    """Equation_Of_Time(JD, year) in hours (SF:1301-1429), vectorised."""
+    e = np.float64(0.016713)
+    eps = np.float64(23.4397) * (np.pi / np.float64(180))
+    dpy = np.float64(365.2425)
+    twopi = np.float64(2) * np.pi
+    Tp = np.array([_perihelion_jd(int(y)) for y in years])
+    M = (twopi / dpy) * (JD - Tp)
+    M = (M + twopi) % twopi
+    VE = np.float64(79.3125) + dpy * (years.astype(np.float64) - np.float64(2000))
+    PT = (np.float64(365) + Tp) - VE
+    L = M + twopi * (PT / dpy)
+    TE = (-2.0 * e * np.sin(M)) + (np.sin(2 * L) * (eps / 2) ** 2.0)
+    return TE / (np.float64(2) * np.pi / np.float64(24))
+
+
+class StepClock:
+    """Uniform scalars for model steps k = 0, 1, 2, ... of one run."""
+
+    def __init__(self, start_time, dt_hours, lat: float, lon: float, time_zone: str | None = None,
+                 ring_len: int = 72):
+        self.start = parse_time(start_time)
+        self.dt = dt_hours
+        self.lat = lat
+        self.lon = lon
+        self.tz = ZoneInfo(time_zone or zone_for(lat, lon))
+        self.ring_len = int(ring_len)
+
+    # -- calendar ----------------------------------------------------------
+    def calendar(self, k0: int, n: int):
+        """(julian_day, year, GMT_offset, TSN_offset) for steps k0..k0+n-1
+        (update_julian_day :957-1004)."""
+        jd = np.empty(n)
+        yr = np.empty(n, dtype=np.int64)
+        gmt = np.empty(n)
+        clock_hour = np.empty(n)
+        utc = ZoneInfo("UTC")
+        for i in range(n):
+            t = self.start + timedelta(hours=self.dt * (k0 + i + 1))
+            J = t.timetuple().tm_yday - 1 + t.hour / 24 + t.minute / 1440 + t.second / 86400
+            jd[i] = J
+            yr[i] = t.year
+            clock_hour[i] = (J - int(J)) * np.float64(24)
+            gmt[i] = t.replace(tzinfo=utc).astimezone(self.tz).utcoffset().total_seconds() / 3600.0
+        LC = ((gmt * np.float64(15)) - self.lon) / np.float64(15)  # SF:1466-1468
+        solar_noon = np.float64(12) + LC + _equation_of_time_hours(jd, yr)  # SF:1471
+        return jd, yr, gmt, clock_hour - solar_noon
+
+    # -- per-step uniforms --------------------------------------------------
+    def uniforms(self, k0: int, n: int, frames=None, hist=None) -> np.ndarray:
+        """tfg_uniforms records for steps k0..k0+n-1.
+
+        frames: forcing frame per step (default 0); hist: output-history slot
+        per step (default 0).  The snowfall-window slot is (k mod ring_len).
+        """
+        jd, _, _, th = self.calendar(k0, n)
+        u = np.zeros(n, dtype=UNIFORM_DTYPE)
+        lat = self.lat
+        G = (2 * np.pi) * jd / np.float64(365)  # Day_Angle SF:176
+        delta = (np.float64(0.006918) - (np.float64(0.399912) * np.cos(G)) + (np.float64(0.070257) * np.sin(G))
+                 - (np.float64(0.006758) * np.cos(np.float64(2) * G)) + (np.float64(0.000907) * np.sin(np.float64(2) * G))
+                 - (np.float64(0.002697) * np.cos(np.float64(3) * G)) + (np.float64(0.001480) * np.sin(np.float64(3) * G)))
+        E0 = (np.float64(1.000110) + (np.float64(0.034221) * np.cos(G)) + (np.float64(0.001280) * np.sin(G))
+              + (np.float64(0.000719) * np.cos(np.float64(2) * G)) + (np.float64(0.000077) * np.sin(np.float64(2) * G)))
+        lat_rad = lat * _RAD
+        # Optical_Air_Mass (Kasten & Young; SF:540-570), gamma clamped >= 0
+        Z = np.arccos(np.sin(lat_rad) * np.sin(delta) + np.cos(lat_rad) * np.cos(delta) * np.cos(_OMEGA * th))
+        gamma = np.maximum(90.0 - Z * (180 / np.pi), 0.0)
+        m_opt = np.float64(1) / (np.sin(gamma * (np.pi / 180)) + 0.50572 / (gamma + 6.07995) ** 1.6364)
+        # ET_Radiation_Flux on the flat (SF:383-413)
+        k_flat = np.float64(1361.5) * E0 * (np.cos(delta) * np.cos(lat_rad) * np.cos(_OMEGA * th)
+                                            + np.sin(delta) * np.sin(lat_rad))
+        k_flat = np.maximum(k_flat, 0.0)
+        # Sunrise/Sunset_Offset at the centroid latitude (SF:319-358)
+        arg = -np.float64(1) * np.tan(lat_rad) * np.tan(delta)
+        arg = np.minimum(np.maximum(-1, arg), 1)
+        flat_sr = -np.float64(1) * np.arccos(arg) / _OMEGA
+        flat_ss = np.arccos(arg) / _OMEGA
+        wth = _OMEGA * th
+        u["th"], u["omega_th"], u["cos_wth"], u["sin_wth"] = th, wth, np.cos(wth), np.sin(wth)
+        u["sin_d"], u["cos_d"], u["tan_d"] = np.sin(delta), np.cos(delta), np.tan(delta)
+        u["isc_e0"] = np.float64(1361.5) * E0
+        u["m_opt"], u["k_et_flat"], u["flat_sr"], u["flat_ss"] = m_opt, k_flat, flat_sr, flat_ss
+        for f32, f64 in FLOAT_COPIES:
+            u[f32] = u[f64].astype(np.float32)
+        u["frame"] = 0 if frames is None else frames
+        u["hist"] = 0 if hist is None else hist
+        u["slot"] = (np.arange(k0, k0 + n) % self.ring_len).astype(np.int32)
+        return u
