@@ -64,20 +64,76 @@ def oracle_run(cfg: dict, static: dict, forcing: dict, nsteps: int | None = None
     return out, m
 
 
-def parity(gpu: np.ndarray, ref: np.ndarray, rtol: float = 1e-5):
-    """Floored relative error |gpu-ref| / max(|ref|, s_v), s_v = p99 |ref|.
+def scale_floor(ref: np.ndarray) -> float:
+    """s_v of SURVEY 8(d): the 99th percentile of |ref|, taken over the
+    non-zero entries so that sparse variables (ice melt is zero almost
+    everywhere) get a meaningful floor."""
+    a = np.abs(np.asarray(ref, dtype=np.float64))
+    a = a[a > 0]
+    return float(np.percentile(a, 99)) if a.size else 0.0
+
+
+def parity(gpu: np.ndarray, ref: np.ndarray, rtol: float = 1e-5, mask=None):
+    """Floored relative error |gpu-ref| / max(|ref|, s_v).
 
     Returns (max floored error, fraction of elements above pure-relative rtol).
+    `mask` (same shape, bool) selects the elements that are compared.
     """
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
-    s_v = float(np.percentile(np.abs(ref), 99)) if ref.size else 0.0
+    s_v = scale_floor(ref)
+    if mask is not None:
+        gpu, ref = gpu[mask], ref[mask]
     floor = np.maximum(np.abs(ref), s_v)
     err = np.abs(gpu - ref)
     with np.errstate(divide="ignore", invalid="ignore"):
         fl = np.where(floor > 0, err / floor, np.where(err > 0, np.inf, 0.0))
         rel = np.where(np.abs(ref) > 0, err / np.abs(ref), np.where(err > 0, np.inf, 0.0))
     return float(np.max(fl)) if fl.size else 0.0, float(np.mean(rel > rtol)) if rel.size else 0.0
+
+
+MELT_OUT_EPS = 1e-9  # m of snow depth: "melt-out" vicinity for the residual-flip rule
+
+
+def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
+    """Cells whose trajectories part at a melt-out residual.
+
+    The reference decides ice melt with ``h_swe == 0 & previous_swe == 0``
+    (bmi_topoflow_glacier.py:1424) on h_swe = max(h - (h/3600)*dt*3600, 0),
+    whose sub-ulp residual is 0 or ~1e-19 depending on the last bit of h.
+    Any engine whose state differs from the reference in the last bit can land
+    on the other side, which switches IM on one step earlier or later.
+    A cell is classified as a flip at step k when (a) it is the cell's first
+    step outside tolerance, (b) the IM on/off gate differs there, and (c) one
+    trajectory has a snow depth within MELT_OUT_EPS of zero at k or k-1.
+    Returns (flip_step per cell or -1, list of genuinely failing (cell, step, var)).
+    """
+    names = [v for v in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") if v in gpu]
+    nsteps, ncell = np.asarray(ref[names[0]]).shape
+    bad = np.zeros((nsteps, ncell), dtype=bool)
+    for v in names:
+        g, r = np.asarray(gpu[v], np.float64), np.asarray(ref[v], np.float64)
+        fl = np.abs(g - r) / np.maximum(np.maximum(np.abs(r), scale_floor(r)), 1e-300)
+        bad |= fl > rtol
+    flip = np.full(ncell, -1)
+    genuine = []
+    for c in np.nonzero(bad.any(axis=0))[0]:
+        k = int(np.argmax(bad[:, c]))
+        gate = (np.asarray(gpu["IM"])[k, c] > 0) != (np.asarray(ref["IM"])[k, c] > 0)
+        ks = [k] + ([k - 1] if k > 0 else [])
+        near = min(min(abs(float(np.asarray(gpu["h_snow"])[j, c])), abs(float(np.asarray(ref["h_snow"])[j, c]))) for j in ks)
+        if gate and near <= MELT_OUT_EPS:
+            flip[c] = k
+        else:
+            genuine.append((int(c), k, [v for v in names if np.abs(np.asarray(gpu[v])[k, c] - np.asarray(ref[v])[k, c])
+                                        > rtol * max(abs(np.asarray(ref[v])[k, c]), scale_floor(ref[v]))]))
+    return flip, genuine
+
+
+def valid_mask(flip: np.ndarray, nsteps: int) -> np.ndarray:
+    """[nsteps][ncell] True where a cell has not yet flipped."""
+    k = np.arange(nsteps)[:, None]
+    return (flip[None, :] < 0) | (k < flip[None, :])
 
 
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
@@ -160,12 +216,15 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     report = {}
     worst = 0.0
     worst_rel = 0.0
+    tol = 1e-5 if engine == "float32" else 1e-10
+    flip, genuine = melt_out_flips(gpu, ref, tol)
+    mask = valid_mask(flip, nsteps)
     for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH"):
-        e, frac = parity(gpu[name], ref[name])
+        e, frac = parity(gpu[name], ref[name], mask=mask)
         report[name] = (e, frac)
         worst = max(worst, e)
     for name in ("h_swe", "h_iwe"):
-        e, frac = parity(gpu[name], ref[name][-1])
+        e, frac = parity(gpu[name], ref[name][-1], mask=flip < 0)
         report[name] = (e, frac)
         worst = max(worst, e)
     dref = np.array([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max])
@@ -173,13 +232,16 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     dg[5] = diag[:, 5].max()
     with np.errstate(divide="ignore", invalid="ignore"):
         drel = np.where(dref != 0, np.abs(dg - dref) / np.abs(dref), np.abs(dg - dref))
-    report["diag"] = (float(np.max(drel)), 0.0)
-    worst_rel = max(worst, float(np.max(drel)))
-    tol = 1e-5 if engine == "float32" else 1e-9
-    ok = worst_rel <= tol
-    summary = ", ".join(f"{k}={v[0]:.2e}" for k, v in report.items())
+    # vol_IM sums IM over all cells including flipped ones: compare P-volumes strictly
+    report["diag"] = (float(np.max(drel[[0, 1, 2, 5]])), 0.0)
+    worst_rel = max(worst, report["diag"][0])
+    n_flip = int((flip >= 0).sum())
+    ok = worst_rel <= tol and not genuine and n_flip <= max(1, int(0.01 * flip.size))
+    summary = ", ".join(f"{k}={v[0]:.2e}" for k, v in report.items()) + f", melt-out flips={n_flip}/{flip.size}"
+    if genuine:
+        summary += f", FAILURES={genuine[:5]}"
     return {"ok": ok, "max_rel": worst_rel, "report": report, "summary": summary, "gpu": gpu, "ref": ref,
-            "diag": dg, "diag_ref": dref}
+            "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine}
 
 
 def ns(**kw):

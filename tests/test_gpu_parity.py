@@ -6,7 +6,11 @@ Tolerances
   fp64 engine : relative 1e-10 vs the reference fixtures (observed ~1e-13;
                 ocml vs numpy SVML libm differ in the last bits).
   fp32 engine : SURVEY 8(d) floored relative 1e-5:
-                |gpu - ref| <= 1e-5 * max(|ref|, p99|ref| of that variable).
+                |gpu - ref| <= 1e-5 * max(|ref|, s_v), s_v = p99 of |ref| over
+                the variable's non-zero values.
+  Melt-out residual flips (tests/harness.py:melt_out_flips) are the one
+  discontinuity a last-bit state difference can toggle; a flipped cell is
+  compared up to its flip step, and flips must stay rare.
 """
 
 import numpy as np
@@ -14,8 +18,8 @@ import pandas as pd
 import pytest
 import yaml
 
-from tests.harness import (BASE_CFG, GOLDEN, OUT_NAMES, gpu_run_fields, load_golden, make_engine, oracle_run,
-                           parity, run_gpu_vs_oracle, synthetic_inputs)
+from tests.harness import (BASE_CFG, GOLDEN, OUT_NAMES, gpu_run_fields, load_golden, make_engine, melt_out_flips,
+                           oracle_run, parity, run_gpu_vs_oracle, synthetic_inputs, valid_mask)
 
 pytestmark = pytest.mark.gpu
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
@@ -153,13 +157,19 @@ def test_fp64_engine_vs_reference_fixtures(name):
     g = load_golden(name)
     n = g["ncell"]
     outs, state, diag = gpu_run_fields(g["cfg"], g["static"], g["forcing"], 1, n, "float64", g["nsteps"])
+    flip, genuine = melt_out_flips(outs, g["outputs"], 1e-10)
+    assert not genuine, genuine
+    assert (flip >= 0).sum() <= max(1, n // 32), flip
+    mask = valid_mask(flip, g["nsteps"])
     for v in HIST:
-        assert _rel(outs[v], g["outputs"][v]) <= 1e-10, v
-    assert _rel(state["h_swe"], g["outputs"]["h_swe"][-1]) <= 1e-10
-    assert _rel(state["h_iwe"], g["outputs"]["h_iwe"][-1]) <= 1e-10
-    assert _rel(state["Eccs"], g["internal"]["Eccs"][-1]) <= 1e-9
-    assert _rel(state["albedo"], g["internal"]["albedo"][-1]) <= 1e-12
-    assert _rel(diag[0, :5], [g["internal"][k][-1].sum() for k in ("vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM")]) <= 1e-10
+        assert parity(outs[v], g["outputs"][v], mask=mask)[0] <= 1e-10, v
+    keep = flip < 0
+    assert parity(state["h_swe"], g["outputs"]["h_swe"][-1], mask=keep)[0] <= 1e-10
+    assert parity(state["h_iwe"], g["outputs"]["h_iwe"][-1], mask=keep)[0] <= 1e-10
+    assert parity(state["Eccs"], g["internal"]["Eccs"][-1], mask=keep)[0] <= 1e-9
+    assert _rel(state["albedo"][keep], g["internal"]["albedo"][-1][keep]) <= 1e-12
+    vols = ("vol_P", "vol_PR", "vol_PS") + (("vol_SM", "vol_IM") if keep.all() else ())
+    assert _rel(diag[0, :len(vols)], [g["internal"][k][-1].sum() for k in vols]) <= 1e-10
     assert diag[0, 5] == g["internal"]["P_max"][-1].max()
 
 
@@ -172,11 +182,15 @@ def test_fp32_engine_vs_oracle_on_fixture_inputs():
     static = {k: r32(v) for k, v in g["static"].items()}
     outs, state, _ = gpu_run_fields(g["cfg"], static, forcing, 8, 8, "float32", g["nsteps"])
     ref, _ = oracle_run(g["cfg"], static, forcing)
+    flip, genuine = melt_out_flips(outs, ref, 1e-5)
+    assert not genuine, genuine
+    assert (flip >= 0).sum() <= 2, flip
+    mask = valid_mask(flip, g["nsteps"])
     for v in HIST:
-        err, frac = parity(outs[v], ref[v])
+        err, frac = parity(outs[v], ref[v], mask=mask)
         assert err <= 1e-5, (v, err, frac)
     for v in ("h_swe", "h_iwe"):
-        err, _ = parity(state[v], ref[v][-1])
+        err, _ = parity(state[v], ref[v][-1], mask=flip < 0)
         assert err <= 1e-5, v
 
 

@@ -80,11 +80,21 @@ _EAGER_MAX_CELLS = 4096
 
 
 def crosswalk_to_external(name: str) -> str:
+    """Reference helper (:93-95); despite its name it maps BMI -> internal."""
     return INTERNAL_NAME_CROSSWALK[name]
 
 
-def crosswalk_to_interal(name: str) -> str:  # reference spelling (:98)
+def crosswalk_to_interal(name: str) -> str:
+    """Reference helper, reference spelling (:98-100); maps internal -> BMI."""
     return EXTERNAL_NAME_CROSSWALK[name]
+
+
+def _ext(internal: str) -> str:
+    return EXTERNAL_NAME_CROSSWALK[internal]
+
+
+def _int(external: str) -> str:
+    return INTERNAL_NAME_CROSSWALK[external]
 
 
 def first_containing(name: str, *states: Context) -> Context:
@@ -180,7 +190,7 @@ class BmiTopoflowGlacier(BmiBase):
         eng.set_field("aspect", np.float64(cfg.aspect))
         for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
             v = np.float64(getattr(cfg, key))
-            self._outputs.set_value(crosswalk_to_external(name), v)
+            self._outputs.set_value(_ext(name), v)
             eng.set_field(name, v)
         eng.init_state()
         self._stale.clear()
@@ -208,9 +218,9 @@ class BmiTopoflowGlacier(BmiBase):
     def _push_inputs(self) -> None:
         eng = self._engine
         for name in _PHYSICS_INPUTS:
-            eng.set_field(name, self._dynamic_inputs.value(crosswalk_to_external(name)))
+            eng.set_field(name, self._dynamic_inputs.value(_ext(name)))
         for name in sorted(self._dirty_outputs):
-            eng.set_field(name, self._outputs.value(crosswalk_to_external(name)))
+            eng.set_field(name, self._outputs.value(_ext(name)))
         self._dirty_outputs.clear()
 
     def _after_steps(self, nsteps: int) -> None:
@@ -219,7 +229,7 @@ class BmiTopoflowGlacier(BmiBase):
         self.julian_day, self.year, self.GMT_offset, self.TSN_offset = float(jd[0]), int(yr[0]), float(gmt[0]), float(tsn[0])
         self.start_datetime = self.start_time + timedelta(hours=self.dt * (k + 1))
         self._timestep += nsteps
-        self._stale = {crosswalk_to_internal_out(n) for n, _ in _output_vars}
+        self._stale = {_int(n) for n, _ in _output_vars}
         if self._eager:
             for name in list(self._stale):
                 self._refresh(name)
@@ -257,14 +267,14 @@ class BmiTopoflowGlacier(BmiBase):
 
     # ------------------------------------------------------------- mirrors
     def _refresh(self, internal: str) -> None:
-        ext = crosswalk_to_external(internal)
+        ext = _ext(internal)
         self._outputs.value(ext)[:] = self._engine.get_field(internal)
         self._stale.discard(internal)
 
     def _mirror(self, external: str) -> np.ndarray:
         ctx = first_containing(external, self._outputs, self._dynamic_inputs)
         if ctx is self._outputs and self._engine is not None:
-            internal = crosswalk_to_interal(external)
+            internal = _int(external)
             if internal in self._stale:
                 self._refresh(internal)
         return ctx.value(external)
@@ -289,7 +299,7 @@ class BmiTopoflowGlacier(BmiBase):
         ctx = first_containing(name, self._outputs, self._dynamic_inputs)
         ctx.set_value(name, src)
         if ctx is self._outputs:
-            internal = crosswalk_to_interal(name)
+            internal = _int(name)
             self._stale.discard(internal)
             self._dirty_outputs.add(internal)
 
@@ -298,7 +308,7 @@ class BmiTopoflowGlacier(BmiBase):
         ctx = first_containing(name, self._outputs, self._dynamic_inputs)
         ctx.set_value_at_indices(name, np.asarray(inds), np.asarray(src))
         if ctx is self._outputs:
-            self._dirty_outputs.add(crosswalk_to_interal(name))
+            self._dirty_outputs.add(_int(name))
 
     def get_value(self, name: str, dest):
         """Copy of a variable, flattened into `dest` (reference :1810-1824)."""
@@ -389,7 +399,3 @@ class BmiTopoflowGlacier(BmiBase):
     Ecci = property(lambda self: self._engine.get_field("Ecci"), doc="ice cold content [J m-2]")
     albedo = property(lambda self: self._engine.get_field("albedo"), doc="surface albedo")
     n = property(lambda self: self._engine.get_field("n"), doc="days since last major snowfall")
-
-
-def crosswalk_to_internal_out(external: str) -> str:
-    return EXTERNAL_NAME_CROSSWALK[external]
