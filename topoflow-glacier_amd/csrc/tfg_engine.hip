@@ -52,17 +52,12 @@ enum { S_HSWE = 0, S_HIWE, S_ECCS, S_ECCI, S_N, S_ALB, S_HSNOW, S_HICE };
 enum { F_P = 0, F_T, F_Q, F_PA, F_UZ };
 enum { H_HSNOW = 0, H_SM, H_HICE, H_IM, H_MTOT, H_RH };
 
+// Scalars of a launch (kernarg).  The buffers are separate __restrict__
+// kernel parameters: that lets the compiler keep the per-step uniforms in
+// scalar registers (s_load) and never order a forcing load behind an output
+// store.
 struct KArgs {
   DevParams p;
-  const void* forc;       // [n_frames][5][n_pad] R
-  const void* stat;       // [3][n_pad] R: elev, slope, aspect
-  const int32_t* catch_id;  // [n_pad] or nullptr
-  double* st;             // [8][n_pad]
-  int64_t* tot;           // [n_pad]
-  int32_t* ring;          // [ring_len][n_pad]
-  void* hist;             // [hist_depth][6][n_pad] R
-  double* slab;           // [gridDim][n_catch][6]
-  const tfg_uniforms* u;  // [K]
   int K;
   int n_catch;
   int64_t n, n_pad;
@@ -127,7 +122,15 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 }
 
 template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
-__global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
+__global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+                                                  const R* __restrict__ forc,      // [n_frames][5][n_pad]
+                                                  const R* __restrict__ stat,      // [3][n_pad]
+                                                  const int32_t* __restrict__ catch_id,  // [n_pad] | null
+                                                  double* __restrict__ st,         // [8][n_pad]
+                                                  int64_t* __restrict__ tot,       // [n_pad]
+                                                  int32_t* __restrict__ ring,      // [ring_len][n_pad]
+                                                  R* __restrict__ hist,            // [hist_depth][6][n_pad]
+                                                  double* __restrict__ slab) {     // [gridDim][n_catch][6]
   extern __shared__ double lds_bins[];  // [kWaves][n_catch][6]
   const DevParams& p = a.p;
   const int nb = a.n_catch * 6;
@@ -140,10 +143,6 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
   const int64_t g0 = (int64_t)blockIdx.x * ngroups / gridDim.x;
   const int64_t g1 = ((int64_t)blockIdx.x + 1) * ngroups / gridDim.x;
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
-  const R* __restrict__ forc = static_cast<const R*>(a.forc);
-  const R* __restrict__ stat = static_cast<const R*>(a.stat);
-  R* __restrict__ hist = static_cast<R*>(a.hist);
-  double* __restrict__ st = a.st;
   using StaticT = typename std::conditional<EXACT, CellStatic, CellStaticF>::type;
 
   CellDiag acc;
@@ -160,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
     }
     if (in) {
       const int64_t c0 = g * C;
-      if constexpr (CATCH) iload<C>(a.catch_id + c0, cid);
+      if constexpr (CATCH) iload<C>(catch_id + c0, cid);
       // static rasters -> per-cell solar geometry (fp64 derivation), once per launch
       StaticT S[C];
       {
@@ -211,24 +210,35 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
           }
         }
         int64_t t[C];
-        lload<C>(a.tot + c0, t);
+        lload<C>(tot + c0, t);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
       }
 
-      for (int k = 0; k < a.K; ++k) {
-        const tfg_uniforms* up = a.u + k;
+      // Software pipeline over the fused steps: the forcing frame and the
+      // expiring window slot of step k+1 are requested before step k is
+      // computed, so their HBM latency overlaps this step's arithmetic.  Two
+      // register sets alternate (loop unrolled by two) so no copy has to wait
+      // for a load in flight, and every request is unconditional (the last
+      // step re-requests its own frame) so the compiler can count loads in
+      // flight instead of draining them at a join.  A one-slot window
+      // (ring_len == 1) runs unfused (tfg_step): its slot read would otherwise
+      // precede the write of the step before.
+      struct Frame { R P[C], T[C], Q[C], PA[C], UZ[C]; int32_t q[C]; };
+      auto fetch = [&](int k, Frame& f) {
+        const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
+        const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad + c0;
+        vload<R, C>(fr + F_P * n_pad, f.P);
+        vload<R, C>(fr + F_T * n_pad, f.T);
+        vload<R, C>(fr + F_Q * n_pad, f.Q);
+        vload<R, C>(fr + F_PA * n_pad, f.PA);
+        vload<R, C>(fr + F_UZ * n_pad, f.UZ);
+        iload<C>(ring + (int64_t)un->slot * n_pad + c0, f.q);
+      };
+      auto advance = [&](int k, const Frame& f) {
+        const tfg_uniforms* up = uni + k;
         const tfg_uniforms u = *up;
-        const R* __restrict__ fr = forc + (int64_t)u.frame * kNumForc * n_pad + c0;
-        R P[C], T[C], Q[C], PA[C], UZ[C];
-        vload<R, C>(fr + F_P * n_pad, P);
-        vload<R, C>(fr + F_T * n_pad, T);
-        vload<R, C>(fr + F_Q * n_pad, Q);
-        vload<R, C>(fr + F_PA * n_pad, PA);
-        vload<R, C>(fr + F_UZ * n_pad, UZ);
-        int32_t* __restrict__ slot = a.ring + (int64_t)u.slot * n_pad + c0;
-        int32_t qo[C], qn[C];
-        iload<C>(slot, qo);
+        int32_t qn[C];
         R o_hs[C], o_sm[C], o_hi[C], o_im[C], o_mt[C], o_rh[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) {
@@ -236,16 +246,16 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
           CellDiag& d = CATCH ? cacc[j] : acc;
           const bool valid = (c0 + j) < a.n;
           if constexpr (EXACT) {
-            tfg::cell_step_exact(p, S[j], u, (double)P[j], (double)T[j], (double)Q[j], (double)PA[j],
-                                 (double)UZ[j], qo[j], qn[j], cs[j], o, d, valid);
+            tfg::cell_step_exact(p, S[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
+                                 (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid);
           } else {
-            tfg::cell_step_fast(p, S[j], up, u, (float)P[j], (float)T[j],
-                                (float)Q[j], (float)PA[j], (float)UZ[j], qo[j], qn[j], cs[j], o, d, valid);
+            tfg::cell_step_fast(p, S[j], up, u, (float)f.P[j], (float)f.T[j], (float)f.Q[j], (float)f.PA[j],
+                                (float)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid);
           }
           o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
           o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
         }
-        istore<C>(slot, qn);
+        istore<C>(ring + (int64_t)u.slot * n_pad + c0, qn);
         R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad + c0;
         vstore<R, C>(h + H_HSNOW * n_pad, o_hs);
         vstore<R, C>(h + H_SM * n_pad, o_sm);
@@ -253,6 +263,14 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
         vstore<R, C>(h + H_IM * n_pad, o_im);
         vstore<R, C>(h + H_MTOT * n_pad, o_mt);
         vstore<R, C>(h + H_RH * n_pad, o_rh);
+      };
+      Frame fa, fb;
+      fetch(0, fa);
+      for (int k = 0; k < a.K; k += 2) {
+        fetch(k + 1, fb);
+        advance(k, fa);
+        fetch(k + 2, fa);
+        if (k + 1 < a.K) advance(k + 1, fb);
       }
       // write back state
       {
@@ -278,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
         int64_t t[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) t[j] = cs[j].tot_q;
-        lstore<C>(a.tot + c0, t);
+        lstore<C>(tot + c0, t);
       }
     }
     if constexpr (CATCH) {
@@ -288,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
   }
   if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
   __syncthreads();
-  double* slab = a.slab + (int64_t)blockIdx.x * nb;
+  double* bslab = slab + (int64_t)blockIdx.x * nb;
   for (int i = threadIdx.x; i < nb; i += kBlock) {
     double v = lds_bins[i];
     if ((i % 6) == 5) {
@@ -296,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a) {
     } else {
       for (int w = 1; w < kWaves; ++w) v += lds_bins[w * nb + i];
     }
-    slab[i] = v;
+    bslab[i] = v;
   }
 }
 
@@ -643,15 +661,6 @@ template <class R, bool EXACT>
 int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds) {
   KArgs a;
   a.p = h->dp;
-  a.forc = h->forc;
-  a.stat = h->stat;
-  a.catch_id = h->catch_id;
-  a.st = h->st;
-  a.tot = h->tot;
-  a.ring = h->ring;
-  a.hist = h->hist;
-  a.slab = h->slab;
-  a.u = d_u;
   a.K = K;
   a.n_catch = h->n_catch;
   a.n = h->n;
@@ -659,10 +668,12 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   const bool rd = !h->depths_derived;
   const bool ct = h->catch_id != nullptr;
   constexpr int C = kCellsPerThread;
-  if (rd && ct) hipLaunchKernelGGL((k_fused<R, EXACT, true, true, C>), blocks, kBlock, lds, h->stream, a);
-  else if (rd) hipLaunchKernelGGL((k_fused<R, EXACT, true, false, C>), blocks, kBlock, lds, h->stream, a);
-  else if (ct) hipLaunchKernelGGL((k_fused<R, EXACT, false, true, C>), blocks, kBlock, lds, h->stream, a);
-  else hipLaunchKernelGGL((k_fused<R, EXACT, false, false, C>), blocks, kBlock, lds, h->stream, a);
+#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, h->slab
+  if (rd && ct) hipLaunchKernelGGL((k_fused<R, EXACT, true, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
+  else if (rd) hipLaunchKernelGGL((k_fused<R, EXACT, true, false, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
+  else if (ct) hipLaunchKernelGGL((k_fused<R, EXACT, false, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
+  else hipLaunchKernelGGL((k_fused<R, EXACT, false, false, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
+#undef TFG_ARGS
   HIPCHK(h, hipGetLastError());
   return TFG_OK;
 }
@@ -930,8 +941,9 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
   const int nb = h->n_catch * 6;
-  for (int64_t k0 = 0; k0 < nsteps; k0 += h->fuse) {
-    const int K = (int)std::min<int64_t>(h->fuse, nsteps - k0);
+  const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
+  for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
+    const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
     int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, h->d_u + k0, K, blocks, lds)
                                     : launch_fused<double, true>(h, h->d_u + k0, K, blocks, lds);
     if (rc) return rc;
