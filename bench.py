@@ -35,7 +35,7 @@ METRIC = "cell-updates/sec (nx·ny·steps) on 8192² fp32 grid; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per cell (DESIGN.md "Bytes per cell-update")
 BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs f32
-BYTES_PER_LAUNCH = 12 + (6 * 8 + 8) * 2  # static 3xf32; state 6xf64 + window total i64, in and out
+BYTES_PER_LAUNCH = 36 + (6 * 8 + 8) * 2  # solar geometry 5xf32+2xf64; state 6xf64 + window total i64, in and out
 
 BASE_CFG = {
     "site_prefix": "synthetic", "forcing_file": "synthetic", "dt": 1, "start_time": "2013032000",

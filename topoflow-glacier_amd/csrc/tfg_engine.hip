@@ -44,6 +44,9 @@ constexpr int kBlock = 256;
 #define TFG_CELLS_PER_THREAD 1
 #endif
 constexpr int kCellsPerThread = TFG_CELLS_PER_THREAD;  // adjacent cells per lane
+#ifndef TFG_PREFETCH_DEPTH
+#define TFG_PREFETCH_DEPTH 1  // time steps of forcing requested ahead
+#endif
 constexpr int kWaves = kBlock / 64;
 constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
 constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
@@ -66,29 +69,41 @@ struct KArgs {
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
 template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
 
+// Every access is (wave-uniform 64-bit field base) + (32-bit per-lane byte
+// offset): the global_load/store "saddr" form, one offset VGPR per element
+// size instead of a 64-bit address per field (tfg_create keeps n_pad*8 < 2^32).
 template <class T, int C>
-__device__ __forceinline__ void vload(const T* __restrict__ p, T (&v)[C]) {
-  const Pack<T, C> x = *reinterpret_cast<const Pack<T, C>*>(p);
+__device__ __forceinline__ void vload(const T* __restrict__ base, uint32_t i, T (&v)[C]) {
+  const uint32_t off = i * (uint32_t)sizeof(T);
+  const Pack<T, C> x = *reinterpret_cast<const Pack<T, C>*>(reinterpret_cast<const char*>(base) + off);
 #pragma unroll
   for (int j = 0; j < C; ++j) v[j] = x.v[j];
 }
 template <class T, int C>
-__device__ __forceinline__ void vstore(T* __restrict__ p, const T (&v)[C]) {
+__device__ __forceinline__ void vstore(T* __restrict__ base, uint32_t i, const T (&v)[C]) {
+  const uint32_t off = i * (uint32_t)sizeof(T);
   Pack<T, C> x;
 #pragma unroll
   for (int j = 0; j < C; ++j) x.v[j] = v[j];
-  *reinterpret_cast<Pack<T, C>*>(p) = x;
+  *reinterpret_cast<Pack<T, C>*>(reinterpret_cast<char*>(base) + off) = x;
 }
-template <int C> __device__ __forceinline__ void dload(const double* p, double (&v)[C]) { vload<double, C>(p, v); }
-template <int C> __device__ __forceinline__ void dstore(double* p, const double (&v)[C]) { vstore<double, C>(p, v); }
-template <int C> __device__ __forceinline__ void iload(const int32_t* p, int32_t (&v)[C]) { vload<int32_t, C>(p, v); }
-template <int C> __device__ __forceinline__ void istore(int32_t* p, const int32_t (&v)[C]) { vstore<int32_t, C>(p, v); }
-template <int C> __device__ __forceinline__ void lload(const int64_t* p, int64_t (&v)[C]) { vload<int64_t, C>(p, v); }
-template <int C> __device__ __forceinline__ void lstore(int64_t* p, const int64_t (&v)[C]) { vstore<int64_t, C>(p, v); }
+template <int C> __device__ __forceinline__ void dload(const double* p, uint32_t i, double (&v)[C]) { vload<double, C>(p, i, v); }
+template <int C> __device__ __forceinline__ void dstore(double* p, uint32_t i, const double (&v)[C]) { vstore<double, C>(p, i, v); }
+template <int C> __device__ __forceinline__ void iload(const int32_t* p, uint32_t i, int32_t (&v)[C]) { vload<int32_t, C>(p, i, v); }
+template <int C> __device__ __forceinline__ void istore(int32_t* p, uint32_t i, const int32_t (&v)[C]) { vstore<int32_t, C>(p, i, v); }
+template <int C> __device__ __forceinline__ void lload(const int64_t* p, uint32_t i, int64_t (&v)[C]) { vload<int64_t, C>(p, i, v); }
+template <int C> __device__ __forceinline__ void lstore(int64_t* p, uint32_t i, const int64_t (&v)[C]) { vstore<int64_t, C>(p, i, v); }
 
 __device__ __forceinline__ void diag_zero(CellDiag& d) {
   d.P = d.PR = d.PS = d.SM = d.IM = 0.0;
   d.Pmax = -INFINITY;
+}
+
+// The fast engine accumulates raw sums of P, P_rain, P_snow, SM, IM and applies
+// the constant factors (da*dt, da*dt*3600; :567, :1486) once per flush.
+__device__ __forceinline__ void diag_scale(CellDiag& d, const DevParams& p) {
+  const double a = p.da_m2 * p.dt, b = p.da_m2 * p.dt * 3600.0;
+  d.P *= a; d.PR *= a; d.PS *= a; d.SM *= b; d.IM *= b;
 }
 
 // Fold the lanes' partial sums into this wave's LDS bins, one pass per
@@ -121,10 +136,14 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
   }
 }
 
+#ifndef TFG_MIN_WAVES
+#define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
+#endif
 template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
-__global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+__global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
+                                                  const float* __restrict__ geo,   // [5][n_pad] f32 + [2][n_pad] f64
                                                   const int32_t* __restrict__ catch_id,  // [n_pad] | null
                                                   double* __restrict__ st,         // [8][n_pad]
                                                   int64_t* __restrict__ tot,       // [n_pad]
@@ -159,47 +178,66 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
     }
     if (in) {
       const int64_t c0 = g * C;
-      if constexpr (CATCH) iload<C>(catch_id + c0, cid);
+      const uint32_t lc = (uint32_t)c0;  // element index within every field
+      if constexpr (CATCH) iload<C>(catch_id, lc, cid);
       // static rasters -> per-cell solar geometry (fp64 derivation), once per launch
       StaticT S[C];
-      {
+      if constexpr (EXACT) {
         R el[C], sl[C], as[C];
-        vload<R, C>(stat + c0, el);
-        vload<R, C>(stat + n_pad + c0, sl);
-        vload<R, C>(stat + 2 * n_pad + c0, as);
+        vload<R, C>(stat, lc, el);
+        vload<R, C>(stat + n_pad, lc, sl);
+        vload<R, C>(stat + 2 * n_pad, lc, as);
+#pragma unroll
+        for (int j = 0; j < C; ++j) S[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
+      } else {
+        // per-cell solar geometry precomputed by k_prepare_geo (fast engine)
+        float g[5][C];
+        double t[2][C];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) vload<float, C>(geo + f * n_pad, lc, g[f]);
+        const double* gd = reinterpret_cast<const double*>(geo + 5 * n_pad);
+        dload<C>(gd, lc, t[0]);
+        dload<C>(gd + n_pad, lc, t[1]);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          if constexpr (EXACT) S[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
-          else S[j] = tfg::derive_static_f(p, (double)el[j], (double)sl[j], (double)as[j]);
+          S[j].elev = g[0][j];
+          S[j].cos_leq = g[1][j];
+          S[j].sin_leq = g[2][j];
+          S[j].cos_dlon = g[3][j];
+          S[j].sin_dlon = g[4][j];
+          S[j].tan_eq = t[0][j];
+          S[j].t_noon = t[1][j];
+          S[j].tan_eq_f = (float)t[0][j];
+          S[j].t_noon_f = (float)t[1][j];
         }
       }
       // state
       CellState cs[C];
       {
         double v[C];
-        dload<C>(st + S_HSWE * n_pad + c0, v);
+        dload<C>(st + S_HSWE * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].h_swe = v[j];
-        dload<C>(st + S_HIWE * n_pad + c0, v);
+        dload<C>(st + S_HIWE * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].h_iwe = v[j];
-        dload<C>(st + S_ECCS * n_pad + c0, v);
+        dload<C>(st + S_ECCS * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].Eccs = v[j];
-        dload<C>(st + S_ECCI * n_pad + c0, v);
+        dload<C>(st + S_ECCI * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].Ecci = v[j];
-        dload<C>(st + S_N * n_pad + c0, v);
+        dload<C>(st + S_N * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].n = v[j];
-        dload<C>(st + S_ALB * n_pad + c0, v);
+        dload<C>(st + S_ALB * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].albedo = v[j];
         if constexpr (READ_DEPTHS) {
-          dload<C>(st + S_HSNOW * n_pad + c0, v);
+          dload<C>(st + S_HSNOW * n_pad, lc, v);
 #pragma unroll
           for (int j = 0; j < C; ++j) cs[j].h_snow = v[j];
-          dload<C>(st + S_HICE * n_pad + c0, v);
+          dload<C>(st + S_HICE * n_pad, lc, v);
 #pragma unroll
           for (int j = 0; j < C; ++j) cs[j].h_ice = v[j];
         } else {
@@ -210,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
           }
         }
         int64_t t[C];
-        lload<C>(tot + c0, t);
+        lload<C>(tot, lc, t);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
       }
@@ -227,13 +265,13 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
       struct Frame { R P[C], T[C], Q[C], PA[C], UZ[C]; int32_t q[C]; };
       auto fetch = [&](int k, Frame& f) {
         const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
-        const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad + c0;
-        vload<R, C>(fr + F_P * n_pad, f.P);
-        vload<R, C>(fr + F_T * n_pad, f.T);
-        vload<R, C>(fr + F_Q * n_pad, f.Q);
-        vload<R, C>(fr + F_PA * n_pad, f.PA);
-        vload<R, C>(fr + F_UZ * n_pad, f.UZ);
-        iload<C>(ring + (int64_t)un->slot * n_pad + c0, f.q);
+        const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad;
+        vload<R, C>(fr + F_P * n_pad, lc, f.P);
+        vload<R, C>(fr + F_T * n_pad, lc, f.T);
+        vload<R, C>(fr + F_Q * n_pad, lc, f.Q);
+        vload<R, C>(fr + F_PA * n_pad, lc, f.PA);
+        vload<R, C>(fr + F_UZ * n_pad, lc, f.UZ);
+        iload<C>(ring + (int64_t)un->slot * n_pad, lc, f.q);
       };
       auto advance = [&](int k, const Frame& f) {
         const tfg_uniforms* up = uni + k;
@@ -255,15 +293,28 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
           o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
           o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
         }
-        istore<C>(ring + (int64_t)u.slot * n_pad + c0, qn);
-        R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad + c0;
-        vstore<R, C>(h + H_HSNOW * n_pad, o_hs);
-        vstore<R, C>(h + H_SM * n_pad, o_sm);
-        vstore<R, C>(h + H_HICE * n_pad, o_hi);
-        vstore<R, C>(h + H_IM * n_pad, o_im);
-        vstore<R, C>(h + H_MTOT * n_pad, o_mt);
-        vstore<R, C>(h + H_RH * n_pad, o_rh);
+        istore<C>(ring + (int64_t)u.slot * n_pad, lc, qn);
+        R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad;
+        vstore<R, C>(h + H_HSNOW * n_pad, lc, o_hs);
+        vstore<R, C>(h + H_SM * n_pad, lc, o_sm);
+        vstore<R, C>(h + H_HICE * n_pad, lc, o_hi);
+        vstore<R, C>(h + H_IM * n_pad, lc, o_im);
+        vstore<R, C>(h + H_MTOT * n_pad, lc, o_mt);
+        vstore<R, C>(h + H_RH * n_pad, lc, o_rh);
       };
+#if TFG_PREFETCH_DEPTH == 2
+      Frame fa, fb, fc;
+      fetch(0, fa);
+      fetch(1, fb);
+      for (int k = 0; k < a.K; k += 3) {
+        fetch(k + 2, fc);
+        advance(k, fa);
+        fetch(k + 3, fa);
+        if (k + 1 < a.K) advance(k + 1, fb);
+        fetch(k + 4, fb);
+        if (k + 2 < a.K) advance(k + 2, fc);
+      }
+#else
       Frame fa, fb;
       fetch(0, fa);
       for (int k = 0; k < a.K; k += 2) {
@@ -272,39 +323,46 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
         fetch(k + 2, fa);
         if (k + 1 < a.K) advance(k + 1, fb);
       }
+#endif
       // write back state
       {
         double v[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].h_swe;
-        dstore<C>(st + S_HSWE * n_pad + c0, v);
+        dstore<C>(st + S_HSWE * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].h_iwe;
-        dstore<C>(st + S_HIWE * n_pad + c0, v);
+        dstore<C>(st + S_HIWE * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].Eccs;
-        dstore<C>(st + S_ECCS * n_pad + c0, v);
+        dstore<C>(st + S_ECCS * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].Ecci;
-        dstore<C>(st + S_ECCI * n_pad + c0, v);
+        dstore<C>(st + S_ECCI * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].n;
-        dstore<C>(st + S_N * n_pad + c0, v);
+        dstore<C>(st + S_N * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].albedo;
-        dstore<C>(st + S_ALB * n_pad + c0, v);
+        dstore<C>(st + S_ALB * n_pad, lc, v);
         int64_t t[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) t[j] = cs[j].tot_q;
-        lstore<C>(tot + c0, t);
+        lstore<C>(tot, lc, t);
       }
     }
     if constexpr (CATCH) {
 #pragma unroll
-      for (int j = 0; j < C; ++j) wave_flush(wbins, cid[j], cacc[j], in);
+      for (int j = 0; j < C; ++j) {
+        if constexpr (!EXACT) diag_scale(cacc[j], p);
+        wave_flush(wbins, cid[j], cacc[j], in);
+      }
     }
   }
-  if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
+  if constexpr (!CATCH) {
+    if constexpr (!EXACT) diag_scale(acc, p);
+    wave_flush(wbins, 0, acc, true);
+  }
   __syncthreads();
   double* bslab = slab + (int64_t)blockIdx.x * nb;
   for (int i = threadIdx.x; i < nb; i += kBlock) {
@@ -315,6 +373,24 @@ __global__ __launch_bounds__(kBlock) void k_fused(const KArgs a, const tfg_unifo
       for (int w = 1; w < kWaves; ++w) v += lds_bins[w * nb + i];
     }
     bslab[i] = v;
+  }
+}
+
+// Per-cell solar geometry of the fast engine, once per static-raster change:
+// [elev, cos(lat_eq), sin(lat_eq), cos(dlon), sin(dlon)] f32, then
+// [tan(eq_lat), t_noon] f64 (tfg::derive_static_f).
+template <class R>
+__global__ void k_prepare_geo(const DevParams p, const R* __restrict__ stat, float* __restrict__ geo, int64_t n_pad) {
+  double* gd = reinterpret_cast<double*>(geo + 5 * n_pad);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
+    const CellStaticF f = tfg::derive_static_f(p, (double)stat[i], (double)stat[n_pad + i], (double)stat[2 * n_pad + i]);
+    geo[i] = f.elev;
+    geo[n_pad + i] = f.cos_leq;
+    geo[2 * n_pad + i] = f.sin_leq;
+    geo[3 * n_pad + i] = f.cos_dlon;
+    geo[4 * n_pad + i] = f.sin_dlon;
+    gd[i] = f.tan_eq;
+    gd[n_pad + i] = f.t_noon;
   }
 }
 
@@ -440,6 +516,8 @@ struct tfg_handle {
   void* forc = nullptr;
   void* stat = nullptr;
   void* lwsw = nullptr;          // [2][n_pad] R, not read by the physics
+  float* geo = nullptr;          // fast engine: [5][n_pad] f32 + [2][n_pad] f64 solar geometry
+  bool geo_dirty = true;
   int32_t* catch_id = nullptr;
   double* st = nullptr;
   int64_t* tot = nullptr;
@@ -668,7 +746,7 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   const bool rd = !h->depths_derived;
   const bool ct = h->catch_id != nullptr;
   constexpr int C = kCellsPerThread;
-#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, h->slab
+#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, h->slab
   if (rd && ct) hipLaunchKernelGGL((k_fused<R, EXACT, true, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
   else if (rd) hipLaunchKernelGGL((k_fused<R, EXACT, true, false, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
   else if (ct) hipLaunchKernelGGL((k_fused<R, EXACT, false, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
@@ -722,6 +800,12 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->nx = nx;
   h->n = ny * nx;
   h->n_pad = round_up(h->n, 64);
+  if (h->n_pad * 8 >= (int64_t)1 << 32) {
+    h->err = "shard too large: ny*nx must stay below 2^29 cells per device (32-bit field offsets)";
+    g_err = h->err;
+    delete h;
+    return TFG_ERR_ARG;
+  }
   h->n_frames = n_frames;
   h->hist_depth = hist_depth;
   h->n_catch = n_catch;
@@ -741,6 +825,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {&h->forc, (size_t)n_frames * kNumForc * np * rs},
       {&h->stat, 3 * (size_t)np * rs},
       {&h->lwsw, 2 * (size_t)np * rs},
+      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (5 * 4 + 2 * 8) : 16},
       {(void**)&h->st, (size_t)kNumState * np * 8},
       {(void**)&h->tot, (size_t)np * 8},
       {(void**)&h->ring, (size_t)p->ring_len * np * 4},
@@ -766,7 +851,7 @@ int tfg_destroy(tfg_handle* h) {
   if (!h) return TFG_OK;
   hipSetDevice(h->device);
   if (h->own_stream) hipStreamSynchronize(h->own_stream);
-  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag,
+  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
   for (void* q : ptrs) if (q) hipFree(q);
   for (int i = 0; i < 2; ++i) {
@@ -843,6 +928,7 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
   }
   int rc = upload(h, dst, fdt, src, src_dtype, n, src_on_device);
   if (rc) return rc;
+  if (field == TFG_ST_ELEV || field == TFG_ST_SLOPE || field == TFG_ST_ASPECT) h->geo_dirty = true;
   if (field == TFG_ST_SLOPE) {
     HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
     if (h->engine == TFG_F32)
@@ -941,6 +1027,12 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
   const int nb = h->n_catch * 6;
+  if (h->engine == TFG_F32 && h->geo_dirty) {
+    hipLaunchKernelGGL((k_prepare_geo<float>), grid_for(h->n_pad), 256, 0, h->stream, h->dp, (const float*)h->stat,
+                       h->geo, h->n_pad);
+    HIPCHK(h, hipGetLastError());
+    h->geo_dirty = false;
+  }
   const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
@@ -998,6 +1090,7 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->slope_invalid = false;
+  h->geo_dirty = true;
   return tfg_init_state(h);
 }
 

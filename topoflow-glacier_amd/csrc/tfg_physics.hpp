@@ -22,6 +22,15 @@
 
 namespace tfg {
 
+// Scheduling fence between physics phases of the fast variant: stops the
+// scheduler from interleaving independent phases, which bounds live ranges
+// (register pressure -> waves per SIMD).  Define TFG_NO_PHASES to disable.
+#ifndef TFG_NO_PHASES
+#define TFG_PHASE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define TFG_PHASE() ((void)0)
+#endif
+
 // ---------------------------------------------------------------------------
 // Constants derived on the host (fp64) from tfg_params, in the reference's
 // association order where it matters.
@@ -181,12 +190,12 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
   SM = npmax(SM, 0.0);
-  // update_SM_integral :1486
-  if (valid) d.SM += SM * p.da_m2 * dt * 3600.0;
+  // update_SM_integral :1486 (FAST: raw sum, scaled by da*dt*3600 at the flush)
+  if (valid) d.SM += FAST ? SM : SM * p.da_m2 * dt * 3600.0;
   // update_swe :1594-1606
   double h_swe = st.h_swe + P_snow * dt;
   double t = npmin(SM * 3600.0, h_swe);
-  SM = t / 3600.0;
+  SM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
   h_swe = h_swe - SM * dt * 3600.0;
   h_swe = npmax(h_swe, 0.0);
   // update_snowfall_cold_content :1507-1537
@@ -207,10 +216,10 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   IM = npmin(IM, FAST ? st.h_iwe * p.inv_dt : st.h_iwe / dt);
   IM = npmax(IM, 0.0);
   // update_IM_integral :1493
-  if (valid) d.IM += IM * p.da_m2 * dt * 3600.0;
+  if (valid) d.IM += FAST ? IM : IM * p.da_m2 * dt * 3600.0;
   // update_iwe :1612-1617
   t = npmin(IM * 3600.0, st.h_iwe);
-  IM = t / 3600.0;
+  IM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
   double h_iwe = st.h_iwe - IM * dt * 3600.0;
   h_iwe = npmax(h_iwe, 0.0);
   // update_combined_meltrate :1441-1443
@@ -435,11 +444,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   const bool is_rain = Td > p.T_rs;
   const double P_rain = is_rain ? Pd : Pd * 0.0;
   const double P_snow = is_rain ? Pd * 0.0 : Pd;
-  if (valid) {
-    d.P += Pd * p.da_m2 * dt;
+  if (valid) {  // raw sums, scaled by da*dt at the flush
+    d.P += Pd;
     d.Pmax = npmax(d.Pmax, Pd);
-    d.PR += P_rain * p.da_m2 * dt;
-    d.PS += P_snow * p.da_m2 * dt;
+    d.PR += P_rain;
+    d.PS += P_snow;
   }
   float e_sat_air;
   if (!p.satterlund) {
@@ -449,6 +458,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   }
   const float e_air = Hum_sp * P_air * frcp(p.f_eps + p.f_one_minus_eps * Hum_sp) * 0.01f;
   const float RH = e_air * frcp(e_sat_air);
+  TFG_PHASE();
   const float log_term = flog(e_air * (1.0f / 6.1121f));
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
   const float T_surf = (h_snow > 0.0 || h_ice > 0.0) ? fminf(T_dew, 0.0f) : T_dew;
@@ -470,10 +480,12 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   const float W_p = 1.12f * fexp(0.0614f * T_dew);
   const float e_surf = RH * e_sat_surf;
   const float Qe = p.f_rho_air_Lv * Dh * (e_air - e_surf) * (p.f_lhc * frcp(p0));
+  TFG_PHASE();
   // albedo with the exact fixed-point window
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
   st.tot_q += (int64_t)q_new - (int64_t)q_old;
   const float albedo = albedo_step<float>(p, st, st.tot_q >= p.thr_q, T_air);
+  TFG_PHASE();
   // clear sky
   const float m_opt = u.m_opt_f;
   const float kf = u.k_et_flat_f;
@@ -504,6 +516,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
     if (dark) K_cs = 0.0f;
   }
   const float Qn_SW = K_cs * (1.0f - albedo);
+  TFG_PHASE();
   float em_air;
   if (!p.satterlund) {
     const float x = e_air * 0.1f * frcp(T_K);
@@ -517,6 +530,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   const float LW_out = p.f_em_surf_sigma * (ts2 * ts2) + p.f_one_minus_em_surf * LW_in;
   const float Qn_LW = LW_in - LW_out;
   const float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
+  TFG_PHASE();
   double T_wb = 0.0;
   if (P_snow > 0.0) {
     const float rh = RH;
