@@ -694,6 +694,7 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.f_sigma = (float)q.sigma;
   p.f_one_minus_em_surf = (float)p.one_minus_em_surf;
   p.f_inv_omega = (float)(1.0 / p.omega);
+  p.f_qfac = (float)(q.dt * p.ws * p.qscale);
   p.inv_dt = 1.0 / q.dt;
   p.inv_dt_rhoLf = 1.0 / (q.dt * p.rho_H2O_Lf);
   p.inv_z0 = 1.0 / q.z0_air;

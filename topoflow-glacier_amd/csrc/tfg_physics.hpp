@@ -63,7 +63,7 @@ struct DevParams {
   // fp32 copies used by the fast variant
   float f_sea_p0, f_negMg_over_R, f_eps, f_one_minus_eps, f_gz, f_kappa, f_inv_z0, f_z;
   float f_rho_air_Cp_air, f_rho_air_Lv, f_lhc, f_dust, f_F, f_one_minus_F_172, f_cloud_term;
-  float f_em_surf_sigma, f_sigma, f_one_minus_em_surf, f_inv_omega;
+  float f_em_surf_sigma, f_sigma, f_one_minus_em_surf, f_inv_omega, f_qfac;
 };
 
 // Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
@@ -179,56 +179,60 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
                                               CellState& st, CellOut& o,
                                               CellDiag& d, bool valid) {
 #pragma clang fp contract(off)
+  // FAST: IEEE max/min (one instruction) instead of numpy's NaN-propagating
+  // forms; identical for every non-NaN input.
+  auto mx = [](double a, double b) { return FAST ? fmax(a, b) : npmax(a, b); };
+  auto mn = [](double a, double b) { return FAST ? fmin(a, b) : npmin(a, b); };
   const double dt = p.dt;
   const double previous_swe = st.h_swe;  // :1566-1571
   // update_snow_meltrate :1364-1373
   double E_in = Q_sum * dt;
-  double E_rem = npmax(E_in - st.Eccs, 0.0);
+  double E_rem = mx(E_in - st.Eccs, 0.0);
   // FAST: value-only divisions become products with host reciprocals; the
   // divisions that decide melt-out residuals (t/3600 below) stay exact.
   double SM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
-  SM = npmax(SM, 0.0);
+  SM = mx(SM, 0.0);
   // update_SM_integral :1486 (FAST: raw sum, scaled by da*dt*3600 at the flush)
   if (valid) d.SM += FAST ? SM : SM * p.da_m2 * dt * 3600.0;
   // update_swe :1594-1606
   double h_swe = st.h_swe + P_snow * dt;
-  double t = npmin(SM * 3600.0, h_swe);
+  double t = mn(SM * 3600.0, h_swe);
   SM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
   h_swe = h_swe - SM * dt * 3600.0;
-  h_swe = npmax(h_swe, 0.0);
+  h_swe = mx(h_swe, 0.0);
   // update_snowfall_cold_content :1507-1537
   double Eccs = st.Eccs;
   if (P_snow > 0.0) {
     const double new_h_snow = (P_snow * dt) * p.ws;
     const double del_T = p.T0 - T_wb;
-    Eccs = npmax(Eccs + p.rho_snow_Cp_snow * new_h_snow * del_T - E_in, 0.0);
+    Eccs = mx(Eccs + p.rho_snow_Cp_snow * new_h_snow * del_T - E_in, 0.0);
   }
   // update_ice_meltrate :1418-1434
-  E_rem = npmax(E_in - st.Ecci, 0.0);
+  E_rem = mx(E_in - st.Ecci, 0.0);
   double IM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
-  IM = npmax(IM, 0.0);
+  IM = mx(IM, 0.0);
   IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
-  double Ecci = npmax(st.Ecci - E_in, 0.0);
+  double Ecci = mx(st.Ecci - E_in, 0.0);
   Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;  // previous-step h_ice
   // enforce_max_ice_meltrate :1473-1480
-  IM = npmin(IM, FAST ? st.h_iwe * p.inv_dt : st.h_iwe / dt);
-  IM = npmax(IM, 0.0);
+  IM = mn(IM, FAST ? st.h_iwe * p.inv_dt : st.h_iwe / dt);
+  IM = mx(IM, 0.0);
   // update_IM_integral :1493
   if (valid) d.IM += FAST ? IM : IM * p.da_m2 * dt * 3600.0;
   // update_iwe :1612-1617
-  t = npmin(IM * 3600.0, st.h_iwe);
+  t = mn(IM * 3600.0, st.h_iwe);
   IM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
   double h_iwe = st.h_iwe - IM * dt * 3600.0;
-  h_iwe = npmax(h_iwe, 0.0);
+  h_iwe = mx(h_iwe, 0.0);
   // update_combined_meltrate :1441-1443
   const double M_total = IM + SM + (FAST ? P_rain * (1.0 / 3600.0) : P_rain / 3600.0);
   // update_snow_depth :1711 / update_ice_depth :1726
   const double h_snow = h_swe * p.ws;
   const double h_ice = h_iwe * p.wi;
   // update_snowpack_cold_content :1556-1558 (new h_snow)
-  Eccs = (P_snow <= 0.0) ? npmax(Eccs - E_in, 0.0) : Eccs;
+  Eccs = (P_snow <= 0.0) ? mx(Eccs - E_in, 0.0) : Eccs;
   Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
 
   st.h_swe = h_swe;
@@ -430,6 +434,26 @@ __device__ __noinline__ bool dark_exact(const DevParams& p, double tan_eq, doubl
   return (up->th <= T_sr) || (up->th >= T_ss);
 }
 
+// atan for the fp32 path: argument reduced to [0, 1] (atan(x) = pi/2 -
+// atan(1/x) above 1), minimax polynomial in z^2 (max rel. error ~1.5e-7).
+__device__ __forceinline__ float fast_atanf(float x) {
+  const float ax = fabsf(x);
+  const bool big = ax > 1.0f;
+  const float z = big ? frcp(ax) : ax;
+  const float t = z * z;
+  float u = 0.00282363896258175373f;
+  u = fmaf(u, t, -0.0159569028764963150f);
+  u = fmaf(u, t, 0.0425049886107444763f);
+  u = fmaf(u, t, -0.0748900920152664185f);
+  u = fmaf(u, t, 0.106347933411598206f);
+  u = fmaf(u, t, -0.142027363181114197f);
+  u = fmaf(u, t, 0.199926957488059998f);
+  u = fmaf(u, t, -0.333331018686294556f);
+  float r = fmaf(z * t, u, z);
+  r = big ? 1.57079632679489662f - r : r;
+  return copysignf(r, x);
+}
+
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf, const tfg_uniforms* __restrict__ up,
                                       const tfg_uniforms& u, float P, float T_air, float Hum_sp,
                                       float P_air, float uz, int32_t q_old, int32_t& q_new,
@@ -481,8 +505,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   const float e_surf = RH * e_sat_surf;
   const float Qe = p.f_rho_air_Lv * Dh * (e_air - e_surf) * (p.f_lhc * frcp(p0));
   TFG_PHASE();
-  // albedo with the exact fixed-point window
-  q_new = window_q(P_snow * dt * p.ws, p.qscale);
+  // albedo with the fixed-point window (slot value rounded from fp32)
+  {
+    const float sq = (is_rain ? 0.0f : P) * p.f_qfac;  // P_snow*dt*ws*2^36
+    q_new = (sq == sq) ? (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f)) : 0;
+  }
   st.tot_q += (int64_t)q_new - (int64_t)q_old;
   const float albedo = albedo_step<float>(p, st, st.tot_q >= p.thr_q, T_air);
   TFG_PHASE();
@@ -534,9 +561,9 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf,
   double T_wb = 0.0;
   if (P_snow > 0.0) {
     const float rh = RH;
-    const float twb = T_air * atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + atanf(T_air + rh) -
-                      atanf(rh - 1.676331f) +
-                      (0.00391838f * (rh * __builtin_sqrtf(rh))) * atanf(0.023101f * rh) - 4.86035f;
+    const float twb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
+                      fast_atanf(rh - 1.676331f) +
+                      (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
     T_wb = (double)twb;
   }
   melt_and_mass<true>(p, (double)Q_sum, P_snow, P_rain, (double)RH, T_wb, st, o, d, valid);
