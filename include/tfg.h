@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 1
+#define TFG_ABI_VERSION 2
 
 /* status codes */
 enum {
@@ -118,13 +118,24 @@ typedef struct tfg_uniforms {
   double k_et_flat;  /* ET_Radiation_Flux(lat, JD, th), clamped >= 0     SF:376 */
   double flat_sr;    /* Sunrise_Offset(lat, delta)                       SF:305 */
   double flat_ss;    /* Sunset_Offset(lat, delta)                        SF:334 */
-  /* fp32 copies of the fields above for the fp32 engine (host-rounded) */
-  float th_f, cos_wth_f, sin_wth_f, sin_d_f, cos_d_f, tan_d_f, isc_e0_f, m_opt_f;
-  float k_et_flat_f, flat_sr_f, flat_ss_f, pad_f;
+  /* fp32 engine: coefficients derived from the fields above in fp64 on the
+   * host, then rounded (Clear_Sky_Radiation SF:904-941 regrouped per step) */
+  float cos_wth_f;   /* cos(omega*th)                                           */
+  float sin_wth_f;   /* sin(omega*th)                                           */
+  float omega_th_f;  /* omega*th                                                */
+  float tan_d_f;     /* tan(declination)                                        */
+  float kc_f;        /* isc_e0*cos(d): K_ET = kc*cos(lat_eq)*cos(w*th+dlon)     */
+  float ks_f;        /* isc_e0*sin(d):        + ks*sin(lat_eq)        SF:867-869 */
+  float k_et_flat_f; /* k_et_flat                                               */
+  float tau_c0, tau_c1; /* tau = exp2(c0 + c1*w) - dust, w = exp(0.0614*T_dew):
+                           log2(e)*(a_sa + b_sa*m_opt) regrouped     SF:606-613 */
+  float gam_c0, gam_c1; /* gam_s = 1 + dust - exp2(c0 + c1*w)        SF:648-655 */
+  float pad_f;
   int32_t frame;     /* forcing frame index this step reads                     */
   int32_t hist;      /* output-history slot this step writes                    */
   int32_t slot;      /* snowfall-window ring slot (step mod ring_len)           */
-  int32_t pad;
+  int32_t flat_dark; /* th <= flat_sr || th >= flat_ss (fp64): dark on the flat
+                        centroid, hence on every slope                SF:939-941 */
 } tfg_uniforms;
 
 typedef struct tfg_handle tfg_handle;

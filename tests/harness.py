@@ -137,11 +137,11 @@ def valid_mask(flip: np.ndarray, nsteps: int) -> np.ndarray:
 
 
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
-                fuse_steps: int = 24):
+                fuse_steps: int = 24, row0: int = 0):
     from topoflow_glacier.engine import GlacierEngine
 
     return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
-                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps)
+                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0)
 
 
 def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,
@@ -188,6 +188,26 @@ def synthetic_inputs(seed: int, ny: int, nx: int, n_frames: int, row0: int = 0):
     return synthetic_cells(seed, cells.reshape(-1), d), d
 
 
+def oracle_synthetic(seed: int, ny: int, nx: int, nsteps: int, n_frames: int = 24, row0: int = 0,
+                     cfg_over: dict | None = None):
+    """The oracle on the synthetic workload (host mirror of the device
+    generator) for rows row0..row0+ny-1 of a grid nx wide."""
+    cfg = dict(BASE_CFG)
+    cfg.update(cfg_over or {})
+    syn, _ = synthetic_inputs(seed, ny, nx, n_frames, row0=row0)
+    frames = np.arange(nsteps) % n_frames
+    forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"],
+              "h0_snow": syn["h_snow"], "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
+    static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
+    return oracle_run(cfg, static, forcing, nsteps)
+
+
+def oracle_diag(m) -> np.ndarray:
+    """[1][6] diagnostics row of an oracle model (vol_P, PR, PS, SM, IM, P_max)."""
+    return np.array([[m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max]], dtype=np.float64)
+
+
 def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", seed: int = 7,
                       n_frames: int = 24, fuse_steps: int = 24, cfg_over: dict | None = None):
     """Device-generated synthetic workload on the GPU vs the oracle on the same
@@ -207,12 +227,7 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
         diag = eng.diagnostics()
     finally:
         eng.close()
-    frames = np.arange(nsteps) % n_frames
-    forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
-    static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"],
-              "h0_snow": syn["h_snow"], "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
-    static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
-    ref, m = oracle_run(cfg, static, forcing, nsteps)
+    ref, m = oracle_synthetic(seed, ny, nx, nsteps, n_frames, cfg_over=cfg_over)
     report = {}
     worst = 0.0
     worst_rel = 0.0

@@ -1,0 +1,69 @@
+"""One rank of the row-block sharded path (launched by torchrun from
+tests/test_sharding.py).  Test infrastructure.
+
+--mode oracle : the rank runs the oracle on its row block (CPU, gloo).
+--mode gpu    : the rank runs the HIP engine on its row block; every rank uses
+                cuda:0 (the test box has one GPU), the diagnostics all-reduce
+                goes over gloo.
+Each rank writes its fields and the all-reduced diagnostics to
+<out>/rank<r>.npz.
+"""
+
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", choices=["oracle", "gpu"], required=True)
+    ap.add_argument("--ny", type=int, required=True)
+    ap.add_argument("--nx", type=int, required=True)
+    ap.add_argument("--steps", type=int, required=True)
+    ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+
+    import torch.distributed as dist
+
+    from topoflow_glacier.sharding import allreduce_diagnostics, row_block
+
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    row0, rows = row_block(a.ny, rank, world)
+    fields = {}
+    if a.mode == "oracle":
+        from tests.harness import oracle_diag, oracle_synthetic
+
+        ref, m = oracle_synthetic(a.seed, rows, a.nx, a.steps, a.frames, row0=row0)
+        diag = oracle_diag(m)
+        fields = {k: np.asarray(ref[k][-1]) for k in ("h_snow", "SM", "IM", "M_total", "RH")}
+    else:
+        from tests.harness import BASE_CFG, make_engine
+        from topoflow_glacier.synthetic import diurnal_table
+
+        eng = make_engine(dict(BASE_CFG), rows, a.nx, "float32", n_frames=a.frames, hist_depth=1,
+                          fuse_steps=24, row0=row0)
+        eng.fill_synthetic(a.seed, diurnal_table(a.frames), nx_global=a.nx)
+        eng.run(a.steps)
+        eng.sync()
+        fields = {k: eng.get_field(k) for k in ("h_snow", "SM", "IM", "M_total", "RH", "h_swe")}
+        diag = eng.diagnostics()
+        eng.close()
+    red = allreduce_diagnostics(diag)
+    np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, diag=diag, reduced=red, **fields)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -283,7 +283,9 @@ def test_catchment_diagnostics():
     for c in range(nc):
         sel = cid == c
         vP = (forcing["P"][:, sel] * da_m2 * 1).sum()
-        assert _rel(diag[c, 0], vP) < 1e-12
+        # fp32 engine: each cell's steps of a launch are summed in fp32 (<= 24
+        # terms, bound 1.4e-6, typically ~1e-8), then in fp64 across cells
+        assert _rel(diag[c, 0], vP) < 1e-6
         assert diag[c, 5] == forcing["P"][:, sel].max()
     assert _rel(diag[:, 3].sum(), m.vol_SM) < 1e-5
     assert _rel(diag[:, 4].sum(), m.vol_IM) < 1e-5

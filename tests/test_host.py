@@ -47,7 +47,10 @@ def test_uniforms_match_oracle_functions():
     assert np.array_equal(u["flat_ss"], O.sunset_offset(c["lat"], delta))
     assert np.array_equal(u["omega_th"], O.earth_angular_velocity() * tsn)
     assert np.array_equal(u["slot"], np.arange(5, 205) % 72)
-    assert np.array_equal(u["th_f"], tsn.astype(np.float32))
+    assert np.array_equal(u["omega_th_f"], (O.earth_angular_velocity() * tsn).astype(np.float32))
+    assert np.array_equal(u["kc_f"], (u["isc_e0"] * u["cos_d"]).astype(np.float32))
+    assert np.array_equal(u["flat_dark"], ((tsn <= u["flat_sr"]) | (tsn >= u["flat_ss"])).astype(np.int32))
+    assert 0 < u["flat_dark"].sum() < len(u)  # the window crosses sunrise and sunset
 
 
 def test_time_zone_lookup_and_errors():
@@ -118,7 +121,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 17
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.tfg_abi_version() == 1
+    assert L.tfg_abi_version() == 2
     assert b"gfx950" in L.tfg_build_info()
 
 
@@ -131,14 +134,14 @@ def test_struct_layouts_match_header(tmp_path):
     src.write_text(
         '#include <stdio.h>\n#include <stddef.h>\n#include "tfg.h"\n'
         "int main(void){printf(\"%zu %zu %zu %zu %zu %zu\\n\", sizeof(tfg_params), offsetof(tfg_params, satterlund),"
-        " sizeof(tfg_uniforms), offsetof(tfg_uniforms, th_f), offsetof(tfg_uniforms, frame), offsetof(tfg_uniforms, slot));return 0;}\n"
+        " sizeof(tfg_uniforms), offsetof(tfg_uniforms, cos_wth_f), offsetof(tfg_uniforms, frame), offsetof(tfg_uniforms, slot));return 0;}\n"
     )
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-std=c99", f"-I{ROOT / 'include'}", str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     U = _native.UNIFORM_DTYPE
     assert got == [ctypes.sizeof(_native.TfgParams), _native.TfgParams.satterlund.offset,
-                   U.itemsize, U.fields["th_f"][1], U.fields["frame"][1], U.fields["slot"][1]]
+                   U.itemsize, U.fields["cos_wth_f"][1], U.fields["frame"][1], U.fields["slot"][1]]
 
 
 def test_no_gpu_fails_loudly():

@@ -72,16 +72,29 @@ template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
 // Every access is (wave-uniform 64-bit field base) + (32-bit per-lane byte
 // offset): the global_load/store "saddr" form, one offset VGPR per element
 // size instead of a 64-bit address per field (tfg_create keeps n_pad*8 < 2^32).
+//
+// TFG_LANE_OFF: re-materialise the 32-bit lane offset at each use (empty asm),
+// so instruction selection, which works per basic block, sees base + zext(off)
+// and picks the saddr form instead of a per-lane 64-bit add.
+#ifndef TFG_LANE_OFF
+#define TFG_LANE_OFF 1
+#endif
+__device__ __forceinline__ uint32_t lane_off(uint32_t off) {
+#if TFG_LANE_OFF
+  asm volatile("" : "+v"(off));
+#endif
+  return off;
+}
 template <class T, int C>
 __device__ __forceinline__ void vload(const T* __restrict__ base, uint32_t i, T (&v)[C]) {
-  const uint32_t off = i * (uint32_t)sizeof(T);
+  const uint32_t off = lane_off(i * (uint32_t)sizeof(T));
   const Pack<T, C> x = *reinterpret_cast<const Pack<T, C>*>(reinterpret_cast<const char*>(base) + off);
 #pragma unroll
   for (int j = 0; j < C; ++j) v[j] = x.v[j];
 }
 template <class T, int C>
 __device__ __forceinline__ void vstore(T* __restrict__ base, uint32_t i, const T (&v)[C]) {
-  const uint32_t off = i * (uint32_t)sizeof(T);
+  const uint32_t off = lane_off(i * (uint32_t)sizeof(T));
   Pack<T, C> x;
 #pragma unroll
   for (int j = 0; j < C; ++j) x.v[j] = v[j];
@@ -97,13 +110,6 @@ template <int C> __device__ __forceinline__ void lstore(int64_t* p, uint32_t i, 
 __device__ __forceinline__ void diag_zero(CellDiag& d) {
   d.P = d.PR = d.PS = d.SM = d.IM = 0.0;
   d.Pmax = -INFINITY;
-}
-
-// The fast engine accumulates raw sums of P, P_rain, P_snow, SM, IM and applies
-// the constant factors (da*dt, da*dt*3600; :567, :1486) once per flush.
-__device__ __forceinline__ void diag_scale(CellDiag& d, const DevParams& p) {
-  const double a = p.da_m2 * p.dt, b = p.da_m2 * p.dt * 3600.0;
-  d.P *= a; d.PR *= a; d.PS *= a; d.SM *= b; d.IM *= b;
 }
 
 // Fold the lanes' partial sums into this wave's LDS bins, one pass per
@@ -143,7 +149,7 @@ template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
 __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
-                                                  const float* __restrict__ geo,   // [5][n_pad] f32 + [2][n_pad] f64
+                                                  const float* __restrict__ geo,   // [kGeoF][n_pad] f32 + [2][n_pad] f64
                                                   const int32_t* __restrict__ catch_id,  // [n_pad] | null
                                                   double* __restrict__ st,         // [8][n_pad]
                                                   int64_t* __restrict__ tot,       // [n_pad]
@@ -162,7 +168,7 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
   const int64_t g0 = (int64_t)blockIdx.x * ngroups / gridDim.x;
   const int64_t g1 = ((int64_t)blockIdx.x + 1) * ngroups / gridDim.x;
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
-  using StaticT = typename std::conditional<EXACT, CellStatic, CellStaticF>::type;
+  const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad);
 
   CellDiag acc;
   diag_zero(acc);
@@ -180,36 +186,23 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
       const int64_t c0 = g * C;
       const uint32_t lc = (uint32_t)c0;  // element index within every field
       if constexpr (CATCH) iload<C>(catch_id, lc, cid);
-      // static rasters -> per-cell solar geometry (fp64 derivation), once per launch
-      StaticT S[C];
+      // static rasters: exact engine derives the geometry in fp64 here; the
+      // fast engine reads the planes k_prepare_geo wrote
+      CellStatic SX[EXACT ? C : 1];
+      tfg::CellStaticF SF[EXACT ? 1 : C];
       if constexpr (EXACT) {
         R el[C], sl[C], as[C];
         vload<R, C>(stat, lc, el);
         vload<R, C>(stat + n_pad, lc, sl);
         vload<R, C>(stat + 2 * n_pad, lc, as);
 #pragma unroll
-        for (int j = 0; j < C; ++j) S[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
+        for (int j = 0; j < C; ++j) SX[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
       } else {
-        // per-cell solar geometry precomputed by k_prepare_geo (fast engine)
-        float g[5][C];
-        double t[2][C];
+        float gv[tfg::kGeoF][C];
 #pragma unroll
-        for (int f = 0; f < 5; ++f) vload<float, C>(geo + f * n_pad, lc, g[f]);
-        const double* gd = reinterpret_cast<const double*>(geo + 5 * n_pad);
-        dload<C>(gd, lc, t[0]);
-        dload<C>(gd + n_pad, lc, t[1]);
+        for (int f = 0; f < tfg::kGeoF; ++f) vload<float, C>(geo + f * n_pad, lc, gv[f]);
 #pragma unroll
-        for (int j = 0; j < C; ++j) {
-          S[j].elev = g[0][j];
-          S[j].cos_leq = g[1][j];
-          S[j].sin_leq = g[2][j];
-          S[j].cos_dlon = g[3][j];
-          S[j].sin_dlon = g[4][j];
-          S[j].tan_eq = t[0][j];
-          S[j].t_noon = t[1][j];
-          S[j].tan_eq_f = (float)t[0][j];
-          S[j].t_noon_f = (float)t[1][j];
-        }
+        for (int j = 0; j < C; ++j) SF[j] = {gv[0][j], gv[1][j], gv[2][j], gv[3][j], gv[4][j]};
       }
       // state
       CellState cs[C];
@@ -252,6 +245,12 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
       }
+      // fast engine: fp32 partial sums of this cell over the launch's steps
+      tfg::DiagF df[EXACT ? 1 : C];
+      if constexpr (!EXACT) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) df[j] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      }
 
       // Software pipeline over the fused steps: the forcing frame and the
       // expiring window slot of step k+1 are requested before step k is
@@ -280,18 +279,21 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
         R o_hs[C], o_sm[C], o_hi[C], o_im[C], o_mt[C], o_rh[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-          CellOut o;
-          CellDiag& d = CATCH ? cacc[j] : acc;
-          const bool valid = (c0 + j) < a.n;
           if constexpr (EXACT) {
-            tfg::cell_step_exact(p, S[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
+            CellOut o;
+            CellDiag& d = CATCH ? cacc[j] : acc;
+            const bool valid = (c0 + j) < a.n;
+            tfg::cell_step_exact(p, SX[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
                                  (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid);
+            o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
+            o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           } else {
-            tfg::cell_step_fast(p, S[j], up, u, (float)f.P[j], (float)f.T[j], (float)f.Q[j], (float)f.PA[j],
-                                (float)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid);
+            tfg::CellOutF o;
+            tfg::cell_step_fast(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j], (float)f.Q[j],
+                                (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j]);
+            o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
+            o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           }
-          o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
-          o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
         }
         istore<C>(ring + (int64_t)u.slot * n_pad, lc, qn);
         R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad;
@@ -324,6 +326,25 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
         if (k + 1 < a.K) advance(k + 1, fb);
       }
 #endif
+      // fast engine: fold the cell's partial sums into the fp64 accumulators
+      // with the constant factors of :567, :585-623, :1486, :1493 (padding
+      // cells excluded)
+      if constexpr (!EXACT) {
+        const double fP = p.da_m2 * p.dt, fSM = p.inv_dt_rhoLf * p.da_m2 * p.dt * 3600.0,
+                     fIM = p.da_m2 * p.dt * 3600.0;
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+          if ((c0 + j) < a.n) {
+            CellDiag& d = CATCH ? cacc[j] : acc;
+            d.P += (double)df[j].P * fP;
+            d.PR += (double)df[j].PR * fP;
+            d.PS += (double)df[j].PS * fP;
+            d.SM += (double)df[j].Erem_s * fSM;
+            d.IM += (double)df[j].IM * fIM;
+            d.Pmax = tfg::npmax(d.Pmax, (double)df[j].Pmax);
+          }
+        }
+      }
       // write back state
       {
         double v[C];
@@ -353,16 +374,10 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
     }
     if constexpr (CATCH) {
 #pragma unroll
-      for (int j = 0; j < C; ++j) {
-        if constexpr (!EXACT) diag_scale(cacc[j], p);
-        wave_flush(wbins, cid[j], cacc[j], in);
-      }
+      for (int j = 0; j < C; ++j) wave_flush(wbins, cid[j], cacc[j], in);
     }
   }
-  if constexpr (!CATCH) {
-    if constexpr (!EXACT) diag_scale(acc, p);
-    wave_flush(wbins, 0, acc, true);
-  }
+  if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
   __syncthreads();
   double* bslab = slab + (int64_t)blockIdx.x * nb;
   for (int i = threadIdx.x; i < nb; i += kBlock) {
@@ -377,20 +392,16 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
 }
 
 // Per-cell solar geometry of the fast engine, once per static-raster change:
-// [elev, cos(lat_eq), sin(lat_eq), cos(dlon), sin(dlon)] f32, then
-// [tan(eq_lat), t_noon] f64 (tfg::derive_static_f).
+// kGeoF fp32 planes then [tan(eq_lat), t_noon] fp64 (tfg::derive_geo).
 template <class R>
 __global__ void k_prepare_geo(const DevParams p, const R* __restrict__ stat, float* __restrict__ geo, int64_t n_pad) {
-  double* gd = reinterpret_cast<double*>(geo + 5 * n_pad);
+  double* gd = reinterpret_cast<double*>(geo + tfg::kGeoF * n_pad);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
-    const CellStaticF f = tfg::derive_static_f(p, (double)stat[i], (double)stat[n_pad + i], (double)stat[2 * n_pad + i]);
-    geo[i] = f.elev;
-    geo[n_pad + i] = f.cos_leq;
-    geo[2 * n_pad + i] = f.sin_leq;
-    geo[3 * n_pad + i] = f.cos_dlon;
-    geo[4 * n_pad + i] = f.sin_dlon;
-    gd[i] = f.tan_eq;
-    gd[n_pad + i] = f.t_noon;
+    const tfg::CellGeo g = tfg::derive_geo(p, (double)stat[i], (double)stat[n_pad + i], (double)stat[2 * n_pad + i]);
+#pragma unroll
+    for (int f = 0; f < tfg::kGeoF; ++f) geo[f * n_pad + i] = g.f[f];
+    gd[i] = g.tan_eq;
+    gd[n_pad + i] = g.t_noon;
   }
 }
 
@@ -675,28 +686,32 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.thr_q = (int64_t)std::ceil(0.03 * 68719476736.0);
   p.satterlund = q.satterlund;
   p.ring_len = q.ring_len;
-  p.f_sea_p0 = (float)q.sea_level_p0;
-  p.f_negMg_over_R = (float)(p.negM_g / q.uni_gas_const);
-  p.f_eps = (float)q.eps;
-  p.f_one_minus_eps = (float)(1.0 - q.eps);
-  p.f_gz = (float)p.gz;
-  p.f_kappa = (float)q.kappa;
-  p.f_inv_z0 = (float)(1.0 / q.z0_air);
-  p.f_z = 10.0f;
-  p.f_rho_air_Cp_air = (float)p.rho_air_Cp_air;
-  p.f_rho_air_Lv = (float)p.rho_air_Lv;
-  p.f_lhc = (float)q.latent_heat_constant;
-  p.f_dust = (float)q.dust_atten;
-  p.f_F = (float)q.canopy_factor;
-  p.f_one_minus_F_172 = (float)p.one_minus_F_172;
-  p.f_cloud_term = (float)p.cloud_term;
-  p.f_em_surf_sigma = (float)p.em_surf_sigma;
-  p.f_sigma = (float)q.sigma;
-  p.f_one_minus_em_surf = (float)p.one_minus_em_surf;
-  p.f_inv_omega = (float)(1.0 / p.omega);
-  p.f_qfac = (float)(q.dt * p.ws * p.qscale);
   p.inv_dt = 1.0 / q.dt;
   p.inv_dt_rhoLf = 1.0 / (q.dt * p.rho_H2O_Lf);
+  p.c_sm3600 = 3600.0 / (q.dt * p.rho_H2O_Lf);
+  p.dt3600 = q.dt * 3600.0;
+  {
+    float t = (float)q.T_rain_snow;  // largest float <= T_rain_snow
+    if ((double)t > q.T_rain_snow) t = std::nextafter(t, -INFINITY);
+    p.f_T_rs_dn = t;
+  }
+  p.f_eps100 = (float)(100.0 * q.eps);
+  p.f_ome100 = (float)(100.0 * (1.0 - q.eps));
+  p.f_gz = (float)p.gz;
+  p.f_z = 10.0f;
+  p.f_inv_z0 = (float)(1.0 / q.z0_air);
+  p.f_k2 = (float)((q.kappa / std::log(2.0)) * (q.kappa / std::log(2.0)));
+  p.f_rho_air_Cp_air = (float)p.rho_air_Cp_air;
+  p.f_qe = (float)(p.rho_air_Lv * q.latent_heat_constant * 100.0 / q.sea_level_p0);
+  p.f_dust = (float)q.dust_atten;
+  p.f_1pdust = (float)(1.0 + q.dust_atten);
+  p.f_ccF = (float)(p.one_minus_F_172 * p.cloud_term);
+  p.f_F = (float)q.canopy_factor;
+  p.f_em_surf_sigma = (float)p.em_surf_sigma;
+  p.f_qfac = (float)(q.dt * p.ws * p.qscale);
+  p.f_dt = (float)q.dt;
+  p.f_T0 = (float)q.T0;
+  p.f_c_eccs = (float)(p.rho_snow_Cp_snow * q.dt * p.ws);
   p.inv_z0 = 1.0 / q.z0_air;
 }
 
@@ -767,7 +782,7 @@ extern "C" {
 int tfg_abi_version(void) { return TFG_ABI_VERSION; }
 
 const char* tfg_build_info(void) {
-  return "libtfg abi=1 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
+  return "libtfg abi=2 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
          "k_diag_reduce, k_fill_synthetic";
 }
 
@@ -826,7 +841,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {&h->forc, (size_t)n_frames * kNumForc * np * rs},
       {&h->stat, 3 * (size_t)np * rs},
       {&h->lwsw, 2 * (size_t)np * rs},
-      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (5 * 4 + 2 * 8) : 16},
+      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (tfg::kGeoF * 4 + 2 * 8) : 16},
       {(void**)&h->st, (size_t)kNumState * np * 8},
       {(void**)&h->tot, (size_t)np * 8},
       {(void**)&h->ring, (size_t)p->ring_len * np * 4},
@@ -850,16 +865,16 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
 
 int tfg_destroy(tfg_handle* h) {
   if (!h) return TFG_OK;
-  hipSetDevice(h->device);
-  if (h->own_stream) hipStreamSynchronize(h->own_stream);
+  (void)hipSetDevice(h->device);
+  if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
-  for (void* q : ptrs) if (q) hipFree(q);
+  for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
-    if (h->h_u[i]) hipHostFree(h->h_u[i]);
-    if (h->h_u_ev[i]) hipEventDestroy(h->h_u_ev[i]);
+    if (h->h_u[i]) (void)hipHostFree(h->h_u[i]);
+    if (h->h_u_ev[i]) (void)hipEventDestroy(h->h_u_ev[i]);
   }
-  if (h->own_stream) hipStreamDestroy(h->own_stream);
+  if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return TFG_OK;
 }

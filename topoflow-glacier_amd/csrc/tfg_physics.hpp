@@ -22,15 +22,6 @@
 
 namespace tfg {
 
-// Scheduling fence between physics phases of the fast variant: stops the
-// scheduler from interleaving independent phases, which bounds live ranges
-// (register pressure -> waves per SIMD).  Define TFG_NO_PHASES to disable.
-#ifndef TFG_NO_PHASES
-#define TFG_PHASE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define TFG_PHASE() ((void)0)
-#endif
-
 // ---------------------------------------------------------------------------
 // Constants derived on the host (fp64) from tfg_params, in the reference's
 // association order where it matters.
@@ -60,10 +51,22 @@ struct DevParams {
   int64_t thr_q;              // ceil(0.03 * 2^36)                 :1040
   int32_t satterlund;
   int32_t ring_len;
-  // fp32 copies used by the fast variant
-  float f_sea_p0, f_negMg_over_R, f_eps, f_one_minus_eps, f_gz, f_kappa, f_inv_z0, f_z;
-  float f_rho_air_Cp_air, f_rho_air_Lv, f_lhc, f_dust, f_F, f_one_minus_F_172, f_cloud_term;
-  float f_em_surf_sigma, f_sigma, f_one_minus_em_surf, f_inv_omega, f_qfac;
+  // fast variant: fp64 folds
+  double c_sm3600;            // 3600/(dt*rho_H2O*Lf): SM*3600 from E_rem     :1368, :1598
+  double dt3600;              // dt*3600                                      :1599, :1615
+  // fast variant: fp32 constants, folded on the host in fp64
+  float f_T_rs_dn;            // largest float <= T_rain_snow (exact T > T_rs test)
+  float f_eps100, f_ome100;   // 100*eps, 100*(1-eps)                        :817-826
+  float f_gz, f_z, f_inv_z0;  // :640, :670
+  float f_k2;                 // (kappa/ln 2)^2                               :670-672
+  float f_rho_air_Cp_air;     // :744
+  float f_qe;                 // rho_air*Lv*lhc*100/sea_p0: Qe = f_qe*Dh*de*exp(Mg elev/(R T))  :931-934, :551-556
+  float f_dust, f_1pdust;     // dust_atten, 1 + dust_atten                  SF:610, SF:652
+  float f_ccF, f_F;           // (1-F)*1.72*(1+0.22C^2), F                    :1167-1175
+  float f_em_surf_sigma;      // em_surf*sigma: Qn_LW = em_s*sigma*(em_air*Ta^4 - Ts^4)  :1231-1248
+  float f_qfac;               // dt*ws*2^36: snowfall-window slot scale
+  float f_dt, f_T0;
+  float f_c_eccs;             // rho_snow*Cp_snow*dt*ws                       :1527-1533
 };
 
 // Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
@@ -173,66 +176,59 @@ __device__ __forceinline__ void slope_sun_offsets(const DevParams& p, const Cell
 // State update after the net energy flux (fp64, reference order).
 // :1566-1731 -- shared by both variants.
 // ---------------------------------------------------------------------------
-template <bool FAST>
 __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, double P_snow,
                                               double P_rain, double RH, double T_wb,
                                               CellState& st, CellOut& o,
                                               CellDiag& d, bool valid) {
 #pragma clang fp contract(off)
-  // FAST: IEEE max/min (one instruction) instead of numpy's NaN-propagating
-  // forms; identical for every non-NaN input.
-  auto mx = [](double a, double b) { return FAST ? fmax(a, b) : npmax(a, b); };
-  auto mn = [](double a, double b) { return FAST ? fmin(a, b) : npmin(a, b); };
   const double dt = p.dt;
   const double previous_swe = st.h_swe;  // :1566-1571
   // update_snow_meltrate :1364-1373
   double E_in = Q_sum * dt;
-  double E_rem = mx(E_in - st.Eccs, 0.0);
-  // FAST: value-only divisions become products with host reciprocals; the
-  // divisions that decide melt-out residuals (t/3600 below) stay exact.
-  double SM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
+  double E_rem = npmax(E_in - st.Eccs, 0.0);
+  double SM = (E_rem / dt) / p.rho_H2O_Lf;
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
-  SM = mx(SM, 0.0);
-  // update_SM_integral :1486 (FAST: raw sum, scaled by da*dt*3600 at the flush)
-  if (valid) d.SM += FAST ? SM : SM * p.da_m2 * dt * 3600.0;
+  SM = npmax(SM, 0.0);
+  // update_SM_integral :1486
+  if (valid) d.SM += SM * p.da_m2 * dt * 3600.0;
   // update_swe :1594-1606
   double h_swe = st.h_swe + P_snow * dt;
-  double t = mn(SM * 3600.0, h_swe);
-  SM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
+  double t = npmin(SM * 3600.0, h_swe);
+  SM = t / 3600.0;
   h_swe = h_swe - SM * dt * 3600.0;
-  h_swe = mx(h_swe, 0.0);
+  h_swe = npmax(h_swe, 0.0);
   // update_snowfall_cold_content :1507-1537
   double Eccs = st.Eccs;
   if (P_snow > 0.0) {
     const double new_h_snow = (P_snow * dt) * p.ws;
     const double del_T = p.T0 - T_wb;
-    Eccs = mx(Eccs + p.rho_snow_Cp_snow * new_h_snow * del_T - E_in, 0.0);
+    Eccs = npmax(Eccs + p.rho_snow_Cp_snow * new_h_snow * del_T - E_in, 0.0);
   }
   // update_ice_meltrate :1418-1434
-  E_rem = mx(E_in - st.Ecci, 0.0);
-  double IM = FAST ? E_rem * p.inv_dt_rhoLf : (E_rem / dt) / p.rho_H2O_Lf;
-  IM = mx(IM, 0.0);
+  E_rem = npmax(E_in - st.Ecci, 0.0);
+  double IM = (E_rem / dt) / p.rho_H2O_Lf;
+  IM = npmax(IM, 0.0);
   IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
-  double Ecci = mx(st.Ecci - E_in, 0.0);
+  double Ecci = npmax(st.Ecci - E_in, 0.0);
   Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;  // previous-step h_ice
   // enforce_max_ice_meltrate :1473-1480
-  IM = mn(IM, FAST ? st.h_iwe * p.inv_dt : st.h_iwe / dt);
-  IM = mx(IM, 0.0);
+  IM = npmin(IM, st.h_iwe / dt);
+  IM = npmax(IM, 0.0);
   // update_IM_integral :1493
-  if (valid) d.IM += FAST ? IM : IM * p.da_m2 * dt * 3600.0;
+  if (valid) d.IM += IM * p.da_m2 * dt * 3600.0;
   // update_iwe :1612-1617
-  t = mn(IM * 3600.0, st.h_iwe);
-  IM = FAST ? t * (1.0 / 3600.0) : t / 3600.0;
+  t = npmin(IM * 3600.0, st.h_iwe);
+  IM = t / 3600.0;
   double h_iwe = st.h_iwe - IM * dt * 3600.0;
-  h_iwe = mx(h_iwe, 0.0);
+  h_iwe = npmax(h_iwe, 0.0);
   // update_combined_meltrate :1441-1443
-  const double M_total = IM + SM + (FAST ? P_rain * (1.0 / 3600.0) : P_rain / 3600.0);
+  const double M_total = IM + SM + P_rain / 3600.0;
   // update_snow_depth :1711 / update_ice_depth :1726
   const double h_snow = h_swe * p.ws;
   const double h_ice = h_iwe * p.wi;
   // update_snowpack_cold_content :1556-1558 (new h_snow)
-  Eccs = (P_snow <= 0.0) ? mx(Eccs - E_in, 0.0) : Eccs;
+  Eccs = (P_snow <= 0.0) ? npmax(Eccs - E_in, 0.0) : Eccs;
   Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
 
   st.h_swe = h_swe;
@@ -249,23 +245,18 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   o.RH = RH;
 }
 
-// Albedo ageing (:1020-1059) given the window predicate.
-__device__ __forceinline__ double albedo_exp(double x) { return exp(x); }
-__device__ __forceinline__ float albedo_exp(float x) { return __expf(x); }
-
-template <class R>
-__device__ __forceinline__ R albedo_step(const DevParams& p, CellState& st, bool wet_window, R T_air) {
+// Albedo ageing (:1020-1059) given the window predicate (exact variant).
+__device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st, bool wet_window, double T_air) {
   // n: where(tot >= .03, 0, n); where(tot < .03, n + days_per_dt, n)
   st.n = wet_window ? 0.0 : st.n + p.days_per_dt;
-  const R r = (T_air > (R)0) ? (R)0.12 : (R)0.05;
-  const R snow_albedo = (R)0.4 + (R)0.44 * albedo_exp((R)(-st.n) * r);
-  double albedo = (st.h_snow > 0.0) ? (double)snow_albedo : st.albedo;
+  const double r = (T_air > 0.0) ? 0.12 : 0.05;
+  const double snow_albedo = 0.4 + 0.44 * exp(-st.n * r);
+  double albedo = (st.h_snow > 0.0) ? snow_albedo : st.albedo;
   if (st.h_snow == 0.0 && st.h_ice > 0.0) albedo = 0.3;
   if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
   st.albedo = albedo;
-  return (R)albedo;
+  return albedo;
 }
-
 
 // ---------------------------------------------------------------------------
 // EXACT variant (fp64, reference order)
@@ -336,7 +327,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // albedo :1023-1059 with the fixed-point window
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
   st.tot_q += (int64_t)q_new - (int64_t)q_old;
-  const double albedo = albedo_step<double>(p, st, st.tot_q >= p.thr_q, T_air);
+  const double albedo = albedo_step(p, st, st.tot_q >= p.thr_q, T_air);
   // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
@@ -377,27 +368,41 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
            ((0.00391838 * pow(RH, 1.5)) * atan(0.023101 * RH)) - 4.86035;
   }
-  melt_and_mass<false>(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
+  melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
 }
 
 // ---------------------------------------------------------------------------
 // FAST variant: fp32 fluxes, fp64 state and predicates
 // ---------------------------------------------------------------------------
+// Per-cell solar geometry of the fast variant (k_prepare_geo, once per static
+// raster change), five fp32 planes:
+//   ek    = (M g / R) * elev * log2(e)        p0 exponent          :551-556
+//   sl    = sin(lat_eq)                                            SF:753-757
+//   cc    = cos(lat_eq) * cos(dlon)                                SF:730-734
+//   cs    = cos(lat_eq) * sin(dlon)
+//   dlon  = Longitude_Offset [rad]
+// plus two fp64 planes tan(lat_eq), t_noon read only by the exact dark test.
+constexpr int kGeoF = 5;
 struct CellStaticF {
-  float elev, cos_leq, sin_leq, cos_dlon, sin_dlon, t_noon_f, tan_eq_f;
-  double tan_eq, t_noon;  // fp64 copies for the near-edge dark test
+  float ek, sl, cc, cs, dlon;
 };
 
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-__device__ __forceinline__ float fexp(float x) { return fexp2(x * 1.4426950408889634f); }
-__device__ __forceinline__ float flog(float x) { return flog2(x) * 0.6931471805599453f; }
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
 
-// fp32 solar geometry of a cell (from derive_static, once per launch)
-__device__ inline CellStaticF derive_static_f(const DevParams& p, double elev, double slope, double aspect) {
+// fp64 derivation of the per-cell geometry (exact trig identities from
+// sin/cos of the slope and aspect angles; derive_static is the reference-order
+// form of the same quantities).
+struct CellGeo {
+  float f[kGeoF];
+  double tan_eq, t_noon;
+};
+__device__ inline CellGeo derive_geo(const DevParams& p, double elev, double slope, double aspect) {
   double sa, ca;
-  sincos(aspect, &ca, &sa);
+  sincos(aspect, &ca, &sa);  // alpha = pi/2 - aspect: cos(alpha) = sin(aspect), sin(alpha) = cos(aspect)
   if (!isfinite(sa) || !isfinite(ca)) { sa = 1.0; ca = 0.0; }
   double sb, cb;
   if (!(slope == slope)) { sb = 0.0; cb = 1.0; }
@@ -407,25 +412,25 @@ __device__ inline CellStaticF derive_static_f(const DevParams& p, double elev, d
   const double cl = sqrt(fmax(1.0 - sl * sl, 0.0));
   const double t = (sb * sa) / (cb * p.cos_lat - sb * p.sin_lat * ca);
   const double rt = 1.0 / sqrt(1.0 + t * t);
-  CellStaticF f;
-  f.elev = (float)elev;
-  f.sin_leq = (float)sl;
-  f.cos_leq = (float)cl;
-  f.cos_dlon = (float)rt;
-  f.sin_dlon = (float)(t * rt);
-  f.t_noon = -1.0 * atan(t) / p.omega;
-  f.tan_eq = sl / cl;
-  f.t_noon_f = (float)f.t_noon;
-  f.tan_eq_f = (float)f.tan_eq;
-  return f;
+  const double dlon = atan(t);
+  CellGeo g;
+  g.f[0] = (float)(-p.negM_g / p.R * elev * 1.4426950408889634);
+  g.f[1] = (float)sl;
+  g.f[2] = (float)(cl * rt);
+  g.f[3] = (float)(cl * t * rt);
+  g.f[4] = (float)dlon;
+  g.tan_eq = sl / cl;
+  g.t_noon = -1.0 * dlon / p.omega;
+  return g;
 }
 
-// Dark test in fp64 (SF:939) for a cell whose fp32 estimate lies within
-// 0.02 h of sunrise/sunset: the reference's Sunrise/Sunset_Offset_Slope in
-// fp64 from the cell's fp64 tan(eq_lat) and noon offset.
-__device__ __noinline__ bool dark_exact(const DevParams& p, double tan_eq, double t_noon,
-                                        const tfg_uniforms* __restrict__ up) {
+// Dark test in fp64 (SF:939) for a cell whose fp32 test lies within its
+// error margin: the reference's Sunrise/Sunset_Offset_Slope from the cell's
+// fp64 tan(eq_lat) and noon offset (read here, on the rare path).
+__device__ __noinline__ bool dark_exact(const DevParams& p, const double* __restrict__ geo_d, int64_t n_pad,
+                                        int64_t i, const tfg_uniforms* __restrict__ up) {
 #pragma clang fp contract(off)
+  const double tan_eq = geo_d[i], t_noon = geo_d[n_pad + i];
   double arg = -1.0 * tan_eq * up->tan_d;
   arg = npmin(npmax(-1.0, arg), 1.0);
   const double ac = acos(arg);
@@ -454,119 +459,179 @@ __device__ __forceinline__ float fast_atanf(float x) {
   return copysignf(r, x);
 }
 
-__device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& sf, const tfg_uniforms* __restrict__ up,
-                                      const tfg_uniforms& u, float P, float T_air, float Hum_sp,
-                                      float P_air, float uz, int32_t q_old, int32_t& q_new,
-                                      CellState& st, CellOut& o, CellDiag& d, bool valid) {
-  const double dt = p.dt;
-  const double h_snow = st.h_snow, h_ice = st.h_ice;
+// h - a*b with the product rounded first, as numpy evaluates it.  At melt-out
+// (a*b ~ h) the residual decides the exact-zero tests of the next step (the IM
+// gate :1424); a fused multiply-add would leave a one-ulp residual of either
+// sign where the reference's rounded product mostly cancels exactly.
+__device__ __forceinline__ double sub_rounded(double h, double a, double b) {
+#pragma clang fp contract(off)
+  return h - a * b;
+}
+__device__ __forceinline__ double add_rounded(double h, double a, double b) {
+#pragma clang fp contract(off)
+  return h + a * b;
+}
+
+// Per-cell partial sums of the fast variant over one launch's steps (fp32;
+// scaled and added to the fp64 accumulators once per cell, padding excluded).
+struct DiagF {
+  float P, PR, PS, Erem_s, IM, Pmax;
+};
+struct CellOutF {
+  float h_snow, SM, h_ice, IM, M_total, RH;
+};
+
+__device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
+                                      const tfg_uniforms& u, const double* __restrict__ geo_d, int64_t n_pad,
+                                      int64_t cell, float P, float T_air, float Hum_sp, float P_air, float uz,
+                                      int32_t q_old, int32_t& q_new, CellState& st, CellOutF& o, DiagF& d) {
+  const bool snow_pos = st.h_snow > 0.0, ice_pos = st.h_ice > 0.0;  // previous-step depths
   const float T_K = T_air + 273.15f;
-  // p0 [mbar] = sea_p0 * exp(-M g elev / (R T_K)) / 100
-  const float p0 = p.f_sea_p0 * 0.01f * fexp(p.f_negMg_over_R * sf.elev * frcp(T_K));
-  const double Pd = (double)P;
-  const double Td = (double)T_air;
-  const bool is_rain = Td > p.T_rs;
-  const double P_rain = is_rain ? Pd : Pd * 0.0;
-  const double P_snow = is_rain ? Pd * 0.0 : Pd;
-  if (valid) {  // raw sums, scaled by da*dt at the flush
-    d.P += Pd;
-    d.Pmax = npmax(d.Pmax, Pd);
-    d.PR += P_rain;
-    d.PS += P_snow;
-  }
-  float e_sat_air;
+  const float rT = frcp(T_K);
+  // rain/snow split (:578-604): T_air > T_rs, exact via the rounded-down threshold
+  const bool is_rain = T_air > p.f_T_rs_dn;
+  const float P_rain = is_rain ? P : P * 0.0f;
+  const float P_snow = is_rain ? P * 0.0f : P;
+  d.P += P;
+  d.Pmax = npmax(d.Pmax, P);
+  d.PR += P_rain;
+  d.PS += P_snow;
+  // vapour pressures [mbar] (:788-826); RH = e_air / e_sat_air (:838)
+  float inv_esat;
   if (!p.satterlund) {
-    e_sat_air = 6.11f * fexp(17.3f * T_air * frcp(T_air + 237.3f));
+    inv_esat = (1.0f / 6.11f) * fexp2((-17.3f * kLog2e) * T_air * frcp(T_air + 237.3f));
   } else {
-    e_sat_air = fexp2((11.4f - 2353.0f * frcp(T_air + 273.15f)) * 3.3219280948873626f) * 0.01f;
+    inv_esat = 100.0f * fexp2((2353.0f * rT - 11.4f) * 3.3219280948873626f);
   }
-  const float e_air = Hum_sp * P_air * frcp(p.f_eps + p.f_one_minus_eps * Hum_sp) * 0.01f;
-  const float RH = e_air * frcp(e_sat_air);
-  TFG_PHASE();
-  const float log_term = flog(e_air * (1.0f / 6.1121f));
+  const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
+  const float RH = e_air * inv_esat;
+  // dew point (:888-893) and surface temperature (:906-910)
+  const float log_term = flog2(e_air) * kLn2 - 1.8102704f;  // ln(e_air / 6.1121)
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
-  const float T_surf = (h_snow > 0.0 || h_ice > 0.0) ? fminf(T_dew, 0.0f) : T_dew;
+  const float T_surf = (snow_pos || ice_pos) ? fminf(T_dew, 0.0f) : T_dew;
   float e_sat_surf;
   if (!p.satterlund) {
-    e_sat_surf = 6.11f * fexp(17.3f * T_surf * frcp(T_surf + 237.3f));
+    e_sat_surf = 6.11f * fexp2((17.3f * kLog2e) * T_surf * frcp(T_surf + 237.3f));
   } else {
-    e_sat_surf = fexp2((11.4f - 2353.0f * frcp(T_surf + 273.15f)) * 3.3219280948873626f) * 0.01f;
+    e_sat_surf = 0.01f * fexp2((11.4f - 2353.0f * frcp(T_surf + 273.15f)) * 3.3219280948873626f);
   }
+  // turbulent fluxes (:640-745, :919-934)
   const float dTs = T_air - T_surf;
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
   const float Ri = p.f_gz * dTs * frcp(bot);
-  const float zr = (float)((p.z - h_snow) * p.inv_z0);
-  const float arg = p.f_kappa * frcp(flog(fmaxf(zr, 0.01f)));
-  const float Dn = uz * (arg * arg);
-  const float Dh = (Ri > 0.0f) ? Dn * frcp(1.0f + 10.0f * Ri) : Dn * (1.0f - 10.0f * Ri);
-  const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
-  const float W_p = 1.12f * fexp(0.0614f * T_dew);
+  const float L2 = flog2(fmaxf((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
+  const float Dn = uz * p.f_k2 * frcp(L2 * L2);
+  const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
   const float e_surf = RH * e_sat_surf;
-  const float Qe = p.f_rho_air_Lv * Dh * (e_air - e_surf) * (p.f_lhc * frcp(p0));
-  TFG_PHASE();
-  // albedo with the fixed-point window (slot value rounded from fp32)
+  const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
+  const float Qe = p.f_qe * Dh * (e_air - e_surf) * fexp2(g.ek * rT);  // lhc / p0 folded
+  // snowfall window + albedo ageing (:1006-1059)
   {
-    const float sq = (is_rain ? 0.0f : P) * p.f_qfac;  // P_snow*dt*ws*2^36
+    const float sq = P_snow * p.f_qfac;  // P_snow*dt*ws*2^36
     q_new = (sq == sq) ? (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f)) : 0;
   }
   st.tot_q += (int64_t)q_new - (int64_t)q_old;
-  const float albedo = albedo_step<float>(p, st, st.tot_q >= p.thr_q, T_air);
-  TFG_PHASE();
-  // clear sky
-  const float m_opt = u.m_opt_f;
-  const float kf = u.k_et_flat_f;
-  const float tau = fminf(fmaxf(fexp((-0.1240f - 0.0207f * W_p) + (-0.0682f - 0.0248f * W_p) * m_opt) - p.f_dust, 0.0f), 1.0f);
-  // cos(omega*th + dlon) = cos(wth)cos(dlon) - sin(wth)sin(dlon)
-  const float cw = u.cos_wth_f * sf.cos_dlon - u.sin_wth_f * sf.sin_dlon;
-  float K_ET = u.isc_e0_f * ((u.cos_d_f * sf.cos_leq) * cw + sf.sin_leq * u.sin_d_f);
-  K_ET = fmaxf(K_ET, 0.0f);
-  const float gam_s = (1.0f - fexp((-0.0363f - 0.0084f * W_p) + (-0.0572f - 0.0173f * W_p) * m_opt)) + p.f_dust;
-  const float K_dif = 0.5f * gam_s * kf;
-  const float K_global = tau * kf + K_dif;
-  const float K_bs = 0.5f * gam_s * albedo * K_global;
-  float K_cs = tau * K_ET + K_dif + K_bs;
-  // dark mask: fp32 estimate, fp64 re-evaluation within 0.02 h of an edge
+  st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
+  float albedo;
   {
-    const float argf = fminf(fmaxf(-sf.tan_eq_f * u.tan_d_f, -1.0f), 1.0f);
-    const float acf = acosf(argf) * p.f_inv_omega;
-    const float th = u.th_f;
-    const float T_srf = fmaxf(sf.t_noon_f - acf, u.flat_sr_f);
-    const float T_ssf = fminf(sf.t_noon_f + acf, u.flat_ss_f);
-    const float m1 = th - T_srf, m2 = T_ssf - th;
+    const float r = (T_air > 0.0f) ? (0.12f * kLog2e) : (0.05f * kLog2e);
+    const float snow_albedo = 0.4f + 0.44f * fexp2(-(float)st.n * r);
+    double a = snow_pos ? (double)snow_albedo : st.albedo;
+    if (st.h_snow == 0.0 && ice_pos) a = 0.3;
+    if (st.h_snow == 0.0 && st.h_ice == 0.0) a = 0.15;
+    st.albedo = a;
+    albedo = (float)a;
+  }
+  // clear-sky shortwave (SF:904-941); W_p = 1.12*w
+  const float w = fexp2((0.0614f * kLog2e) * T_dew);
+  const float tau = fminf(fmaxf(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);
+  const float gam_s = p.f_1pdust - fexp2(fmaf(u.gam_c1, w, u.gam_c0));
+  // cos(lat_eq)*cos(omega*th + dlon)
+  const float cwl = u.cos_wth_f * g.cc - u.sin_wth_f * g.cs;
+  const float K_ET = fmaxf(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);
+  const float kf = u.k_et_flat_f;
+  const float K_dif = 0.5f * gam_s * kf;
+  const float K_bs = 0.5f * gam_s * albedo * fmaf(tau, kf, K_dif);
+  float K_cs = tau * K_ET + K_dif + K_bs;
+  // dark (SF:939-941): with x = omega*th + dlon and ac = acos(clip(-tan(lat_eq) tan(d))),
+  // th <= T_sr or th >= T_ss  <=>  flat_dark or |x| >= ac
+  //                           <=>  flat_dark or |x| > pi or cos(lat_eq) cos(x) <= -sin(lat_eq) tan(d).
+  // Within the fp32 error margins the fp64 reference form decides.
+  {
+    const float dv = fmaf(g.sl, u.tan_d_f, cwl);
+    const float ax = fabsf(u.omega_th_f + g.dlon);
+    const float mpi = ax - 3.14159265358979f;
     bool dark;
-    if (fabsf(m1) < 0.02f || fabsf(m2) < 0.02f || !(m1 == m1) || !(m2 == m2)) {
-      dark = dark_exact(p, sf.tan_eq, sf.t_noon, up);
+    if (!(fabsf(dv) >= 1e-5f) || !(fabsf(mpi) >= 1e-4f)) {
+      dark = dark_exact(p, geo_d, n_pad, cell, up);
     } else {
-      dark = (m1 <= 0.0f) || (m2 <= 0.0f);
+      dark = (u.flat_dark != 0) || (mpi > 0.0f) || (dv <= 0.0f);
     }
     if (dark) K_cs = 0.0f;
   }
   const float Qn_SW = K_cs * (1.0f - albedo);
-  TFG_PHASE();
+  // longwave (:1167-1248)
   float em_air;
   if (!p.satterlund) {
-    const float x = e_air * 0.1f * frcp(T_K);
-    em_air = p.f_one_minus_F_172 * fexp2(flog2(x) * (1.0f / 7.0f)) * p.f_cloud_term + p.f_F;
+    em_air = fmaf(p.f_ccF, fexp2(flog2(e_air * 0.1f * rT) * (1.0f / 7.0f)), p.f_F);
   } else {
-    em_air = 1.08f * (1.0f - fexp(-fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
+    em_air = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
   }
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
-  const float LW_in = em_air * p.f_sigma * (ta2 * ta2);
-  const float LW_out = p.f_em_surf_sigma * (ts2 * ts2) + p.f_one_minus_em_surf * LW_in;
-  const float Qn_LW = LW_in - LW_out;
+  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air, ta2 * ta2, -(ts2 * ts2));
   const float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
-  TFG_PHASE();
-  double T_wb = 0.0;
-  if (P_snow > 0.0) {
+
+  // ---- state update (:1566-1731), fp64 where depths and cold contents accumulate
+  const double previous_swe = st.h_swe;
+  const double E_in = (double)(Q_sum * p.f_dt);
+  // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
+  const double E_rem_s = fmax(E_in - st.Eccs, 0.0);
+  d.Erem_s += (float)E_rem_s;
+  // update_swe (:1594-1606)
+  double h_swe = add_rounded(st.h_swe, (double)P_snow, p.dt);
+  const double ts = fmin(E_rem_s * p.c_sm3600, h_swe);
+  const double SM = ts * (1.0 / 3600.0);
+  h_swe = fmax(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
+  // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
+  double Eccs = st.Eccs;
+  const bool snowing = P_snow > 0.0f;
+  if (snowing) {
     const float rh = RH;
-    const float twb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
-                      fast_atanf(rh - 1.676331f) +
-                      (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
-    T_wb = (double)twb;
+    const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
+                       fast_atanf(rh - 1.676331f) +
+                       (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
+    Eccs = fmax(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
   }
-  melt_and_mass<true>(p, (double)Q_sum, P_snow, P_rain, (double)RH, T_wb, st, o, d, valid);
+  // ice melt (:1418-1434), cap (:1473-1480), integral (:1493), update_iwe (:1612-1617)
+  const double E_rem_i = fmax(E_in - st.Ecci, 0.0);
+  double IM = (h_swe == 0.0 && previous_swe == 0.0) ? E_rem_i * p.inv_dt_rhoLf : 0.0;
+  double Ecci = fmax(st.Ecci - E_in, 0.0);
+  Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;
+  IM = fmin(IM, st.h_iwe * p.inv_dt);
+  d.IM += (float)IM;
+  const double ti = fmin(IM * 3600.0, st.h_iwe);
+  IM = ti * (1.0 / 3600.0);
+  const double h_iwe = fmax(sub_rounded(st.h_iwe, IM, p.dt3600), 0.0);
+  // depths (:1711, :1726), snowpack cold content (:1556-1558, new h_snow)
+  const double h_snow = h_swe * p.ws;
+  const double h_ice = h_iwe * p.wi;
+  if (!snowing) Eccs = fmax(Eccs - E_in, 0.0);
+  Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
+  st.h_swe = h_swe;
+  st.h_iwe = h_iwe;
+  st.Eccs = Eccs;
+  st.Ecci = Ecci;
+  st.h_snow = h_snow;
+  st.h_ice = h_ice;
+  const float SMf = (float)SM, IMf = (float)IM;
+  o.h_snow = (float)h_snow;
+  o.h_ice = (float)h_ice;
+  o.SM = SMf;
+  o.IM = IMf;
+  o.M_total = IMf + SMf + P_rain * (1.0f / 3600.0f);  // :1441-1443
+  o.RH = RH;
 }
 
 }  // namespace tfg

@@ -54,13 +54,12 @@ class TfgParams(ctypes.Structure):
 # tfg_uniforms, one record per time step (numpy structured dtype, C layout)
 _U_D = ["th", "omega_th", "cos_wth", "sin_wth", "sin_d", "cos_d", "tan_d", "isc_e0", "m_opt",
         "k_et_flat", "flat_sr", "flat_ss"]
-_U_F = ["th_f", "cos_wth_f", "sin_wth_f", "sin_d_f", "cos_d_f", "tan_d_f", "isc_e0_f", "m_opt_f",
-        "k_et_flat_f", "flat_sr_f", "flat_ss_f", "pad_f"]
+_U_F = ["cos_wth_f", "sin_wth_f", "omega_th_f", "tan_d_f", "kc_f", "ks_f", "k_et_flat_f",
+        "tau_c0", "tau_c1", "gam_c0", "gam_c1", "pad_f"]
 UNIFORM_DTYPE = np.dtype(
     [(n, "<f8") for n in _U_D] + [(n, "<f4") for n in _U_F]
-    + [("frame", "<i4"), ("hist", "<i4"), ("slot", "<i4"), ("pad", "<i4")]
+    + [("frame", "<i4"), ("hist", "<i4"), ("slot", "<i4"), ("flat_dark", "<i4")]
 )
-FLOAT_COPIES = list(zip(_U_F[:-1], ["th", "cos_wth", "sin_wth", "sin_d", "cos_d", "tan_d", "isc_e0", "m_opt", "k_et_flat", "flat_sr", "flat_ss"]))
 
 _lib = None
 
@@ -101,8 +100,8 @@ def load() -> ctypes.CDLL:
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    if L.tfg_abi_version() != 1:
-        raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != 1")
+    if L.tfg_abi_version() != 2:
+        raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != 2 (rebuild the library)")
     _lib = L
     return L
 

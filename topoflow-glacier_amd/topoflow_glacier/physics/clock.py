@@ -23,7 +23,7 @@ from zoneinfo import ZoneInfo
 
 import numpy as np
 
-from .._native import FLOAT_COPIES, UNIFORM_DTYPE
+from .._native import UNIFORM_DTYPE
 
 __all__ = ["StepClock", "zone_for", "parse_time", "PERIHELION"]
 
@@ -165,8 +165,19 @@ class StepClock:
         u["sin_d"], u["cos_d"], u["tan_d"] = np.sin(delta), np.cos(delta), np.tan(delta)
         u["isc_e0"] = np.float64(1361.5) * E0
         u["m_opt"], u["k_et_flat"], u["flat_sr"], u["flat_ss"] = m_opt, k_flat, flat_sr, flat_ss
-        for f32, f64 in FLOAT_COPIES:
-            u[f32] = u[f64].astype(np.float32)
+        # fp32-engine coefficients (tfg.h): fp64 here, rounded once
+        log2e = np.float64(1.4426950408889634)
+        u["cos_wth_f"], u["sin_wth_f"], u["omega_th_f"] = u["cos_wth"], u["sin_wth"], wth
+        u["tan_d_f"] = u["tan_d"]
+        u["kc_f"] = u["isc_e0"] * u["cos_d"]
+        u["ks_f"] = u["isc_e0"] * u["sin_d"]
+        u["k_et_flat_f"] = k_flat
+        # a + b*m_opt with a, b affine in W_p = 1.12*w (SF:606-613, SF:648-655)
+        u["tau_c0"] = log2e * (-0.1240 - 0.0682 * m_opt)
+        u["tau_c1"] = log2e * 1.12 * (-0.0207 - 0.0248 * m_opt)
+        u["gam_c0"] = log2e * (-0.0363 - 0.0572 * m_opt)
+        u["gam_c1"] = log2e * 1.12 * (-0.0084 - 0.0173 * m_opt)
+        u["flat_dark"] = ((th <= flat_sr) | (th >= flat_ss)).astype(np.int32)
         u["frame"] = 0 if frames is None else frames
         u["hist"] = 0 if hist is None else hist
         u["slot"] = (np.arange(k0, k0 + n) % self.ring_len).astype(np.int32)
