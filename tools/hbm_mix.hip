@@ -1,0 +1,100 @@
+// hbm_mix -- HBM bandwidth ceiling for the fused kernel's access mix on MI355X.
+//
+// Streams `cells` fp32 elements per plane: each "step" a thread reads R planes
+// and writes W planes at its cell (coalesced, 4 B per lane per plane), the
+// k_fused pattern (R = 6: five forcing fields + window slot; W = 7: window slot
+// + six outputs).  Reports GB/s for several (R, W) mixes so the measured
+// k_fused rate can be placed against what this read/write mix can reach.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
+//   tools/hbm_mix [cells=67108864] [steps=24]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } } while (0)
+
+template <int V> struct Vec;
+template <> struct Vec<1> { using T = float; };
+template <> struct Vec<2> { using T = float2; };
+template <> struct Vec<4> { using T = float4; };
+__device__ __forceinline__ float hsum(float v) { return v; }
+__device__ __forceinline__ float hsum(float2 v) { return v.x + v.y; }
+__device__ __forceinline__ float hsum(float4 v) { return v.x + v.y + v.z + v.w; }
+__device__ __forceinline__ void splat(float& o, float a) { o = a; }
+__device__ __forceinline__ void splat(float2& o, float a) { o = make_float2(a, a + 1.0f); }
+__device__ __forceinline__ void splat(float4& o, float a) { o = make_float4(a, a + 1.0f, a + 2.0f, a + 3.0f); }
+
+// V floats (V adjacent cells) per lane per plane
+template <int R, int W, int V>
+__global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
+                                             int steps, int frames) {
+  using T = typename Vec<V>::T;
+  const uint32_t nv = n / V;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
+    float acc = 0.0f;
+    for (int s = 0; s < steps; ++s) {
+      const T* fin = reinterpret_cast<const T*>(in + (size_t)(s % frames) * R * n);
+      T v[R > 0 ? R : 1];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = fin[(size_t)r * nv + i];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc += hsum(v[r]);
+      T* fo = reinterpret_cast<T*>(out + (size_t)(s % frames) * W * n);
+#pragma unroll
+      for (int w = 0; w < W; ++w) { T o; splat(o, acc + (float)w); fo[(size_t)w * nv + i] = o; }
+    }
+    if (W == 0 && acc == -1.0f) out[i] = acc;  // keep the reads alive
+  }
+}
+
+template <int R, int W, int V = 1>
+void run(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  const int blocks = 256 * 8;
+  k_mix<R, W, V><<<blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    CHECK(hipEventRecord(a));
+    k_mix<R, W, V><<<blocks, 256>>>(in, out, n, steps, frames);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  const double bytes = (double)n * steps * 4.0 * (R + W);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"bytes_per_lane\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, 4 * V, bytes / (best * 1e-3) / 1e9, best);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+}
+
+int main(int argc, char** argv) {
+  const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
+  const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
+  const int frames = steps;  // one distinct frame per step, as k_fused (no address is touched twice)
+  float *in, *out;
+  CHECK(hipMalloc(&in, (size_t)n * 4 * 7 * frames));
+  CHECK(hipMalloc(&out, (size_t)n * 4 * 7 * frames));
+  CHECK(hipMemset(in, 0, (size_t)n * 4 * 7 * frames));
+  CHECK(hipMemset(out, 0, (size_t)n * 4 * 7 * frames));
+  run<6, 7>("k_fused step mix (6 read, 7 write)", in, out, n, steps, frames);
+  run<7, 0>("read only (7 planes)", in, out, n, steps, frames);
+  run<0, 7>("write only (7 planes)", in, out, n, steps, frames);
+  run<1, 1>("copy (1 read, 1 write)", in, out, n, steps, frames);
+  run<6, 1>("read-heavy (6 read, 1 write)", in, out, n, steps, frames);
+  run<6, 7, 2>("k_fused step mix, 8 B/lane", in, out, n, steps, frames);
+  run<6, 7, 4>("k_fused step mix, 16 B/lane", in, out, n, steps, frames);
+  run<7, 0, 4>("read only, 16 B/lane", in, out, n, steps, frames);
+  run<0, 7, 4>("write only, 16 B/lane", in, out, n, steps, frames);
+  run<1, 1, 4>("copy, 16 B/lane", in, out, n, steps, frames);
+  CHECK(hipFree(in));
+  CHECK(hipFree(out));
+  return 0;
+}
