@@ -6,10 +6,13 @@ bmi_topoflow_glacier.py:413-465) applied to every cell of the grid: read that
 hour's forcing frame from HBM, run the fused energy/mass balance, write the six
 BMI outputs of the step to HBM.  Steps are fused `--fuse` per kernel launch
 (state stays in registers between fused steps; every step still streams its
-forcing in and its outputs out).
+forcing in and its outputs out, to its own history slot: hist_depth = fuse, so
+no output write can be absorbed by a cache rewrite).
 
 Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
-HBM-resident frames, fp32 engine (fp64 state).  --gpus N: one process per GPU
+HBM-resident frames, fp32 engine (fp64 state), 96 steps per launch (HBM
+footprint ~210 GB of the 288 GB: 24 forcing frames 32 GB, 96 output slots
+155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).  --gpus N: one process per GPU
 (torchrun), row-block shards of 8192 rows each (weak scaling, no data-path
 collective); value = all cells of all ranks x steps / max-over-ranks time.
 
@@ -48,12 +51,12 @@ BASE_CFG = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=240)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--steps", type=int, default=480)
+    ap.add_argument("--warmup", type=int, default=96)
     ap.add_argument("--ny", type=int, default=8192, help="rows per GPU (weak) or global rows (strong)")
     ap.add_argument("--nx", type=int, default=8192)
     ap.add_argument("--frames", type=int, default=24)
-    ap.add_argument("--fuse", type=int, default=24)
+    ap.add_argument("--fuse", type=int, default=96, help="steps per launch (= output history slots)")
     ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=20251001)
