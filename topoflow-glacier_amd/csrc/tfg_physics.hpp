@@ -390,7 +390,49 @@ struct CellStaticF {
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// log2 with the argument split as m * 2^e, m in [0.5, 1): v_log_f32 then only
+// sees m, whose result is in [-1, 0), so its mean error of -0.44 ulp of the
+// result stays ~1e-8 absolute instead of a relative bias on the whole log.
+// Used where the flux integrates into the state (energy bias accumulates).
+#ifndef TFG_SPLIT_LOG
+#define TFG_SPLIT_LOG 0
+#endif
+__device__ __forceinline__ float flog2_nr(float x);
+__device__ __forceinline__ float flog2_split(float x) {
+#if TFG_LOG_NEWTON >= 2
+  return flog2_nr(x);
+#elif TFG_SPLIT_LOG
+  const float m = __builtin_amdgcn_frexp_mantf(x);
+  const int e = __builtin_amdgcn_frexp_expf(x);
+  return (float)e + flog2(m);
+#else
+  return flog2(x);
+#endif
+}
+// log2 refined by one Newton step on exp2 (v_exp_f32 is unbiased; v_log_f32
+// has a mean error of -0.44 ulp of its result): y += (x*2^-y - 1)*log2(e).
+// The residual error is second order, so no bias reaches the state.
+__device__ __forceinline__ float flog2_nr(float x) {
+  const float y = flog2(x);
+  return fmaf(fmaf(x, fexp2(-y), -1.0f), 1.4426950408889634f, y);
+}
+#ifndef TFG_LOG_NEWTON
+#define TFG_LOG_NEWTON 1  // 0: none, 1: dew point, 2: dew point, Dn and em_air
+#endif
 constexpr float kLog2e = 1.4426950408889634f;
+// expm1 without cancellation: Taylor polynomial (degree 8) for |x| < 0.5
+// (truncation < 1e-8 relative), exp2(x log2 e) - 1 beyond.
+__device__ __forceinline__ float fexpm1(float x) {
+  float q = 1.0f / 40320.0f;
+  q = fmaf(q, x, 1.0f / 5040.0f);
+  q = fmaf(q, x, 1.0f / 720.0f);
+  q = fmaf(q, x, 1.0f / 120.0f);
+  q = fmaf(q, x, 1.0f / 24.0f);
+  q = fmaf(q, x, 1.0f / 6.0f);
+  q = fmaf(q, x, 0.5f);
+  const float small = fmaf(q * x, x, x);
+  return fabsf(x) < 0.5f ? small : fexp2(x * kLog2e) - 1.0f;
+}
 constexpr float kLn2 = 0.6931471805599453f;
 
 // fp64 derivation of the per-cell geometry (exact trig identities from
@@ -497,35 +539,59 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   d.PR += P_rain;
   d.PS += P_snow;
   // vapour pressures [mbar] (:788-826); RH = e_air / e_sat_air (:838)
+  // Brutsaert: e_sat = 6.11 exp(17.3 T/(T+237.3)); Satterlund: 10^(11.4-2353/T_K)/100
+  const float rA = p.satterlund ? rT : frcp(T_air + 237.3f);
   float inv_esat;
   if (!p.satterlund) {
-    inv_esat = (1.0f / 6.11f) * fexp2((-17.3f * kLog2e) * T_air * frcp(T_air + 237.3f));
+    inv_esat = (1.0f / 6.11f) * fexp2((-17.3f * kLog2e) * T_air * rA);
   } else {
     inv_esat = 100.0f * fexp2((2353.0f * rT - 11.4f) * 3.3219280948873626f);
   }
   const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
   const float RH = e_air * inv_esat;
   // dew point (:888-893) and surface temperature (:906-910)
-  const float log_term = flog2(e_air) * kLn2 - 1.8102704f;  // ln(e_air / 6.1121)
+  // ln(e_air / 6.1121) as the log of the ratio (~1): v_log_f32's mean error is
+  // -0.44 ulp of its result, so a result near zero keeps that bias negligible,
+  // where log2(e_air) - log2(6.1121) would carry it into T_dew
+#ifndef TFG_DEW_RATIO
+#define TFG_DEW_RATIO 1
+#endif
+#if TFG_DEW_RATIO && TFG_LOG_NEWTON >= 1
+  const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
+#elif TFG_DEW_RATIO
+  const float log_term = flog2(e_air * (1.0f / 6.1121f)) * kLn2;
+#else
+  const float log_term = flog2(e_air) * kLn2 - 1.8102704f;
+#endif
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
   const float T_surf = (snow_pos || ice_pos) ? fminf(T_dew, 0.0f) : T_dew;
-  float e_sat_surf;
-  if (!p.satterlund) {
-    e_sat_surf = 6.11f * fexp2((17.3f * kLog2e) * T_surf * frcp(T_surf + 237.3f));
-  } else {
-    e_sat_surf = 0.01f * fexp2((11.4f - 2353.0f * frcp(T_surf + 273.15f)) * 3.3219280948873626f);
-  }
   // turbulent fluxes (:640-745, :919-934)
   const float dTs = T_air - T_surf;
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
   const float Ri = p.f_gz * dTs * frcp(bot);
-  const float L2 = flog2(fmaxf((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
+  const float L2 = flog2_split(fmaxf((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
   const float Dn = uz * p.f_k2 * frcp(L2 * L2);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
-  const float e_surf = RH * e_sat_surf;
+  // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
+  // (:853), written without the cancellation of the two near-equal pressures:
+  //   e_air - e_surf = -e_air*expm1(x),  x = -k*dTs/((T_s+c)(T_a+c))
+  // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15)
+  const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
+#ifndef TFG_DE_EXPM1
+#define TFG_DE_EXPM1 0
+#endif
+#if TFG_DE_EXPM1
+  const float xs = (p.satterlund ? -5417.9857f : -4105.29f) * dTs * rS * rA;
+  const float de = -e_air * fexpm1(xs);
+#else
+  // one unbiased exp2 of the exponent difference: the remaining error is
+  // random (v_exp_f32 rounding), not a bias that would accumulate in Eccs
+  const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;  // k*log2(e)
+  const float de = fmaf(-e_air, fexp2(xs2), e_air);
+#endif
   const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
-  const float Qe = p.f_qe * Dh * (e_air - e_surf) * fexp2(g.ek * rT);  // lhc / p0 folded
+  const float Qe = p.f_qe * Dh * de * fexp2(g.ek * rT);  // lhc / p0 folded
   // snowfall window + albedo ageing (:1006-1059)
   {
     const float sq = P_snow * p.f_qfac;  // P_snow*dt*ws*2^36
@@ -574,7 +640,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // longwave (:1167-1248)
   float em_air;
   if (!p.satterlund) {
-    em_air = fmaf(p.f_ccF, fexp2(flog2(e_air * 0.1f * rT) * (1.0f / 7.0f)), p.f_F);
+    em_air = fmaf(p.f_ccF, fexp2(flog2_split(e_air * 0.1f * rT) * (1.0f / 7.0f)), p.f_F);
   } else {
     em_air = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
   }
@@ -632,6 +698,10 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   o.IM = IMf;
   o.M_total = IMf + SMf + P_rain * (1.0f / 3600.0f);  // :1441-1443
   o.RH = RH;
+#if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
+  const float dbg[13] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
+  o.RH = dbg[TFG_DEBUG_TERM];
+#endif
 }
 
 }  // namespace tfg
