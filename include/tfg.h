@@ -78,8 +78,13 @@ enum {
   TFG_ST_ECCS = 19,   /* snowpack cold content  (:392, :1496-1564)           */
   TFG_ST_ECCI = 20,   /* ice cold content       (:394, :1375-1434)           */
   TFG_ST_ALBEDO = 21, /* albedo                 (:369, :1006-1059)           */
-  TFG_ST_NDAYS = 22,  /* days since major snowfall, as a step count (:1040)  */
-  TFG_NUM_FIELDS = 23
+  TFG_ST_NDAYS = 22,  /* days since major snowfall (:1040)                   */
+  /* snowfall window (checkpoint / restart): slot `index` (0..ring_len-1) in
+   * metres of snow, P_snow*dt*ws of one step (:1027-1033); step k writes slot
+   * k mod ring_len.  Setting a slot rebuilds the running total before the
+   * next tfg_step. */
+  TFG_ST_WINDOW = 23,
+  TFG_NUM_FIELDS = 24
 };
 
 /* Diagnostics per catchment, in this order (:558-624, :1482-1494). */

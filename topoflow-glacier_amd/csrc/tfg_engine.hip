@@ -517,6 +517,24 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // ===========================================================================
 // Handle
 // ===========================================================================
+// Snowfall-window checkpoint I/O (TFG_ST_WINDOW): metres <-> fixed point, and
+// the running total rebuilt from the slots.
+__global__ void k_window_set(int32_t* __restrict__ slot, const double* __restrict__ v, int64_t n, double qscale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    slot[i] = tfg::window_q(v[i], qscale);
+}
+__global__ void k_window_get(double* __restrict__ v, const int32_t* __restrict__ slot, int64_t n, double inv_qscale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    v[i] = (double)slot[i] * inv_qscale;
+}
+__global__ void k_window_total(int64_t* __restrict__ tot, const int32_t* __restrict__ ring, int ring_len, int64_t n_pad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t t = 0;
+    for (int s = 0; s < ring_len; ++s) t += ring[(int64_t)s * n_pad + i];
+    tot[i] = t;
+  }
+}
+
 struct tfg_handle {
   int device = 0, engine = TFG_F32;
   int64_t ny = 0, nx = 0, n = 0, n_pad = 0;
@@ -551,6 +569,8 @@ struct tfg_handle {
   bool depths_derived = false;
   bool slope_invalid = false;
   bool initialised = false;
+  bool tot_dirty = false;        // window slots set through TFG_ST_WINDOW
+  double* wtmp = nullptr;        // [n_pad] f64 scratch for window I/O
   int64_t last_hist = 0;
   std::string err;
 };
@@ -867,7 +887,7 @@ int tfg_destroy(tfg_handle* h) {
   if (!h) return TFG_OK;
   (void)hipSetDevice(h->device);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
-  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag,
+  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
@@ -925,6 +945,17 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     return TFG_OK;
   }
   if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  if (field == TFG_ST_WINDOW) {
+    if (index < 0 || index >= h->ring_len) return fail(h, TFG_ERR_ARG, "window slot out of range");
+    if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
+    int rc = upload(h, h->wtmp, TFG_F64, src, src_dtype, n, src_on_device);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_window_set, grid_for(n), 256, 0, h->stream, h->ring + (int64_t)index * h->n_pad, h->wtmp, n,
+                       h->dp.qscale);
+    HIPCHK(h, hipGetLastError());
+    h->tot_dirty = true;
+    return TFG_OK;
+  }
   int fdt = 0;
   void* dst = field_ptr(h, field, index, &fdt);
   if (!dst) return fail(h, TFG_ERR_ARG, "unknown field id " + std::to_string(field));
@@ -975,6 +1006,14 @@ int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype,
     return TFG_OK;
   }
   if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+  if (field == TFG_ST_WINDOW) {
+    if (index < 0 || index >= h->ring_len) return fail(h, TFG_ERR_ARG, "window slot out of range");
+    if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
+    hipLaunchKernelGGL(k_window_get, grid_for(n), 256, 0, h->stream, h->wtmp, h->ring + (int64_t)index * h->n_pad, n,
+                       1.0 / h->dp.qscale);
+    HIPCHK(h, hipGetLastError());
+    return download(h, dst, dst_dtype, h->wtmp, TFG_F64, n, dst_on_device);
+  }
   int fdt = 0;
   const void* src = field_ptr(h, field, index, &fdt);
   if (!src) return fail(h, TFG_ERR_ARG, "unknown field id " + std::to_string(field));
@@ -1000,6 +1039,7 @@ int tfg_init_state(tfg_handle* h) {
   HIPCHK(h, hipMemsetAsync(h->diag, 0, (size_t)h->n_catch * 6 * 8, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->depths_derived = false;
+  h->tot_dirty = false;
   h->initialised = true;
   return TFG_OK;
 }
@@ -1016,6 +1056,11 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
     if (u[k].slot < 0 || u[k].slot >= h->ring_len) return fail(h, TFG_ERR_ARG, "uniforms: ring slot out of range");
   }
   HIPCHK(h, hipSetDevice(h->device));
+  if (h->tot_dirty) {  // window slots were set: rebuild the running totals
+    hipLaunchKernelGGL(k_window_total, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->ring, h->ring_len, h->n_pad);
+    HIPCHK(h, hipGetLastError());
+    h->tot_dirty = false;
+  }
   // stage uniforms: pinned double buffer -> device array
   const int b = h->h_u_next;
   h->h_u_next ^= 1;

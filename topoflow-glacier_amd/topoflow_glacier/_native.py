@@ -28,7 +28,7 @@ FIELD = {
     "LW_in": 0, "P_air": 1, "Hum_sp": 2, "P": 3, "SW_in": 4, "T_air": 5, "uz": 6,
     "h_snow": 7, "h_swe": 8, "SM": 9, "h_ice": 10, "h_iwe": 11, "IM": 12, "M_total": 13, "RH": 14,
     "elev": 15, "slope": 16, "aspect": 17, "catch_id": 18,
-    "Eccs": 19, "Ecci": 20, "albedo": 21, "n": 22,
+    "Eccs": 19, "Ecci": 20, "albedo": 21, "n": 22, "window": 23,
 }
 DIAG_NAMES = ["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"]
 
