@@ -1,0 +1,91 @@
+"""The callers on either side of the melt update:
+forcing ingestion with the reference driver's unit conversions, the mock
+routing, and the single-catchment driver in both of its modes."""
+
+from __future__ import annotations
+
+import numpy as np
+import pytest
+import yaml
+
+from tests.harness import BASE_CFG, GOLDEN, load_golden
+
+CSV = GOLDEN / "sample-cat-3062920.csv"
+
+
+def test_forcing_csv_matches_the_reference_driver_inputs():
+    """The seven per-step inputs equal, bit for bit, what the reference's
+    examples/run_topoflow_glacier.py fed set_value() in the golden run
+    (tests/golden/make_golden.py recorded them)."""
+    from topoflow_glacier.forcing import read_forcing_csv
+
+    g = load_golden("cat3062920_265")
+    t = read_forcing_csv(CSV, BASE_CFG["start_time"], BASE_CFG["end_time"])
+    assert len(t) == g["nsteps"] == 265
+    for name, ref in g["forcing"].items():
+        np.testing.assert_array_equal(t.inputs[name], ref[:, 0], err_msg=name)
+    assert str(t.times[0])[:13] == "2013-03-20T00" and str(t.times[-1])[:13] == "2013-03-31T00"
+
+
+def test_forcing_csv_window_and_errors(tmp_path):
+    from topoflow_glacier.forcing import INTERNAL, frames_from_table, read_forcing_csv
+
+    t = read_forcing_csv(CSV)  # no window: every row
+    assert len(t) == 288
+    s = t.step(5)
+    assert set(s) == set(INTERNAL.values()) and s["wind_speed_UV"] == t.inputs["uz"][5]
+    fr = frames_from_table(t, ncell=3)
+    assert fr["P"].shape == (288, 3) and np.array_equal(fr["P"][:, 2], t.inputs["P"])
+    bad = tmp_path / "bad.csv"
+    bad.write_text("Time,RAINRATE\n2013-03-20 00:00:00,0.0\n")
+    with pytest.raises(KeyError):
+        read_forcing_csv(bad)
+
+
+def test_boxcar_route_is_the_20_step_moving_average():
+    from topoflow_glacier.routing import boxcar_route
+
+    rng = np.random.default_rng(3)
+    x = rng.random(300)
+    y = boxcar_route(x)
+    ref = np.array([sum(0.05 * x[i - j] for j in range(min(i, 19) + 1)) for i in range(len(x))])
+    np.testing.assert_allclose(y, ref, rtol=1e-14, atol=0)
+    assert np.array_equal(boxcar_route(np.stack([x, 2 * x], 1))[:, 0], y)
+    # causal: an impulse spreads over the next 20 steps only
+    imp = np.zeros(50)
+    imp[10] = 1.0
+    r = boxcar_route(imp)
+    assert np.all(r[:10] == 0) and np.allclose(r[10:30], 0.05) and np.all(r[30:] == 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["bmi", "bulk"])
+def test_run_catchment_reproduces_the_reference_runoff(tmp_path, mode):
+    """examples/run_topoflow_glacier.py end to end: runoff [m3 s-1] against the
+    reference's golden tests/data/output_m_total.npy (integration_test.py:151-153)."""
+    from topoflow_glacier.run import run_catchment
+
+    cfg = tmp_path / "cat.yaml"
+    cfg.write_text(yaml.dump(BASE_CFG))
+    r = run_catchment(cfg, forcing=CSV, mode=mode)
+    ref = np.load(GOLDEN / "ref_output_m_total.npy")
+    assert r["runoff"].shape == ref.shape
+    rel = np.abs(r["runoff"] - ref) / np.maximum(np.abs(ref), 1e-300)
+    assert np.all(np.where(ref != 0, rel, np.abs(r["runoff"])) <= 1e-10)
+    g = load_golden("cat3062920_265")
+    assert abs(r["h_swe"][-1] - g["outputs"]["h_swe"][-1, 0]) <= 1e-10 * abs(g["outputs"]["h_swe"][-1, 0])
+
+
+@pytest.mark.gpu
+def test_bulk_mode_equals_per_step_bmi(tmp_path):
+    """Uploading the window as frames and fusing the steps changes nothing."""
+    from topoflow_glacier.run import run_catchment
+
+    cfg = tmp_path / "cat.yaml"
+    cfg.write_text(yaml.dump(BASE_CFG))
+    a = run_catchment(cfg, forcing=CSV, mode="bmi")
+    b = run_catchment(cfg, forcing=CSV, mode="bulk")
+    for k in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH"):
+        assert np.array_equal(a[k], b[k]), k
+    assert a["h_swe"][-1] == b["h_swe"][-1] and a["h_iwe"][-1] == b["h_iwe"][-1]
+    assert np.array_equal(a["routed"], b["routed"])

@@ -115,6 +115,34 @@ def _accessor(external: str, ctx: str):
     return property(getter, setter, doc=f"BMI variable {external}")
 
 
+def make_engine(cfg, n_frames: int = 1, hist_depth: int = 1) -> GlacierEngine:
+    """The device shard a config describes (fp64 engine for one cell, fp32 for grids)."""
+    engine = cfg.engine or ("float64" if cfg.ny * cfg.nx == 1 else "float32")
+    return GlacierEngine(cfg, cfg.ny, cfg.nx, engine=engine, device=cfg.device, n_frames=n_frames,
+                         hist_depth=hist_depth, fuse_steps=cfg.fuse_steps)
+
+
+def configure_engine(eng: GlacierEngine, cfg) -> bool:
+    """initialize()'s static and state setup (:274-411) on an engine: terrain
+    from the YAML scalars, initial depths, cold contents, albedo, window.
+    Returns True when the slope is out of range: the reference then logs,
+    leaves beta unset, and its first update() fails (:1106-1111)."""
+    eng.set_field("elev", np.float64(cfg.elev))
+    beta_invalid = False
+    try:
+        eng.set_field("slope", np.float64(cfg.slope))
+    except nat.NativeError as e:
+        if e.code != nat.ERR_DOMAIN:
+            raise
+        logger.error("ERROR: In met_base.py, some slope angles are out of range.  Returning without setting beta.")
+        beta_invalid = True
+    eng.set_field("aspect", np.float64(cfg.aspect))
+    for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
+        eng.set_field(name, np.float64(getattr(cfg, key)))
+    eng.init_state()
+    return beta_invalid
+
+
 class BmiTopoflowGlacier(BmiBase):
     """BMI composition wrapper for TopoflowGlacier on MI355X."""
 
@@ -173,26 +201,10 @@ class BmiTopoflowGlacier(BmiBase):
         self._dynamic_inputs = build_context(_dynamic_input_vars, n)
         self._outputs = build_context(_output_vars, n)
         self._eager = n <= _EAGER_MAX_CELLS
-        engine = cfg.engine or ("float64" if n == 1 else "float32")
-        self._engine = GlacierEngine(cfg, self.ny, self.nx, engine=engine, device=cfg.device,
-                                     fuse_steps=cfg.fuse_steps)
-        eng = self._engine
-        eng.set_field("elev", np.float64(cfg.elev))
-        try:
-            eng.set_field("slope", np.float64(cfg.slope))
-            self._beta_invalid = False
-        except nat.NativeError as e:
-            if e.code != nat.ERR_DOMAIN:
-                raise
-            # reference: logs and leaves beta unset; the first update() then fails (:1106-1111)
-            logger.error("ERROR: In met_base.py, some slope angles are out of range.  Returning without setting beta.")
-            self._beta_invalid = True
-        eng.set_field("aspect", np.float64(cfg.aspect))
+        self._engine = make_engine(cfg)
+        self._beta_invalid = configure_engine(self._engine, cfg)
         for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
-            v = np.float64(getattr(cfg, key))
-            self._outputs.set_value(_ext(name), v)
-            eng.set_field(name, v)
-        eng.init_state()
+            self._outputs.set_value(_ext(name), np.float64(getattr(cfg, key)))
         self._stale.clear()
         self._dirty_outputs: set[str] = set()
         self._timestep = 0
