@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=24)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-fed forcing) leg")
+    ap.add_argument("--dt", type=float, default=1.0, help="time step [h] (BASELINE config 5: 0.25)")
+    ap.add_argument("--catchments", type=int, default=0,
+                    help="K > 0: per-catchment mass balance over a K-catchment block raster (BASELINE config 5)")
     return ap.parse_args()
 
 
@@ -83,9 +86,10 @@ def cpu_baseline(args, gpu_sample):
     static = dict(elev=syn["elev"], slope=syn["slope"], aspect=syn["aspect"], h0_snow=syn["h_snow"],
                   h0_ice=syn["h_ice"], h0_swe=syn["h_swe"], h0_iwe=syn["h_iwe"])
     static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
-    clock = O.oracle_clock(BASE_CFG["start_time"], BASE_CFG["dt"], steps, BASE_CFG["lon"])
+    cfg = dict(BASE_CFG, dt=args.dt)
+    clock = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
     t0 = time.perf_counter()
-    out, _ = O.run_oracle(BASE_CFG, static, forcing, steps, clock=(clock[0], clock[3]))
+    out, _ = O.run_oracle(cfg, static, forcing, steps, clock=(clock[0], clock[3]))
     dt = time.perf_counter() - t0
     parity = None
     if gpu_sample is not None:
@@ -98,6 +102,14 @@ def cpu_baseline(args, gpu_sample):
     return {"value": n * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
             "sample": f"oracle/tfg_oracle.py (numpy fp64 restatement of update(), single thread) on the first "
                       f"{n} cells x {steps} hourly steps of the same synthetic workload ({dt:.1f} s)"}, parity
+
+
+def catchment_blocks(row0, rows, ny_global, nx, k):
+    """Global block raster of k catchments (8 x 8 blocks, ids mod k), this
+    shard's rows; the per-catchment reduction path of the kernel."""
+    r = (np.arange(row0, row0 + rows) * 8 // max(ny_global, 1))[:, None]
+    c = (np.arange(nx) * 8 // nx)[None, :]
+    return ((r * 8 + c) % k).astype(np.int32).reshape(-1)
 
 
 def pcie_inclusive(eng, args, torch):
@@ -150,10 +162,13 @@ def main():
     else:
         ny_global = args.ny
         row0, rows = row_block(args.ny, rank, world)
-    cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx))
+    cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
+    n_catch = args.catchments + 1 if args.catchments > 0 else 1
     eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
-                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0)
+                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
     eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
+    if args.catchments > 0:
+        eng.set_field("catch_id", catchment_blocks(row0, rows, ny_global, args.nx, args.catchments))
     stream = torch.cuda.Stream(local)  # a real (non-null) stream shared by the engine and the events
     torch.cuda.set_stream(stream)
     eng.set_stream(stream.cuda_stream)
@@ -201,7 +216,7 @@ def main():
         if not args.no_cpu_baseline:
             # a short GPU run on the same sample cells for a parity spot check
             n = min(args.cpu_cells, cells)
-            scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n))
+            scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n, dt=args.dt))
             se = GlacierEngine(scfg, 1, n, engine=args.engine, device=local, n_frames=args.frames,
                                hist_depth=1, fuse_steps=args.fuse)
             se.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=n)
@@ -228,8 +243,9 @@ def main():
             "dtype": "f32" if args.engine == "float32" else "f64",
             "data": "synthetic (counter-hash DEM/forcing with CSV statistics, 24 HBM-resident hourly frames)",
             "config": {
-                "workload": f"{ny_global}x{args.nx} grid ({rows}x{args.nx} per GPU), hourly steps, "
-                            f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch",
+                "workload": f"{ny_global}x{args.nx} grid ({rows}x{args.nx} per GPU), {args.dt:g} h steps, "
+                            f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch"
+                            + (f", {args.catchments} catchments" if args.catchments else ""),
                 "grid_per_gpu": [rows, args.nx],
                 "frames": args.frames,
                 "fuse_steps": args.fuse,
