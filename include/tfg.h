@@ -215,6 +215,22 @@ int tfg_sync(tfg_handle* h);
 int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_global,
                        const float* diurnal, int n_frames);
 
+/* Terrain from a DEM (extension): slope (tan beta) and
+ * aspect rasters from the handle's elevation raster by Horn's 3x3 finite
+ * differences, fp64.  The reference takes both as YAML scalars (config.py:19,
+ * :28) and uses them through set_slope_angle / set_aspect_angle (:1082-1113);
+ * aspect here is the downslope direction in radians counter-clockwise from
+ * east, the quantity those functions turn into alpha = pi/2 - aspect.
+ *   dx, dy      cell size [m]; rows run north to south, columns west to east
+ *   halo_north  elevation row just north of this shard's first row (nx values),
+ *   halo_south  ... just south of its last row; NULL at the domain edge (the
+ *               edge row is replicated, as are the first/last columns)
+ *   halo_dtype  TFG_F32 / TFG_F64; halo_on_device != 0: device pointers
+ * Row-block shards exchange these one-row halos (topoflow_glacier/sharding.py,
+ * RCCL over xGMI); the sharded result equals the unsharded one. */
+int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_north, const void* halo_south,
+                         int halo_dtype, int halo_on_device);
+
 /* Last error message of a handle (NULL: the last create/global error). */
 const char* tfg_last_error(const tfg_handle* h);
 

@@ -259,5 +259,32 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
             "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine}
 
 
+def terrain_dem(ny: int, nx: int) -> np.ndarray:
+    """A smooth synthetic DEM [m] (hills and a tilted plane) on 30 m cells, fp32-exact."""
+    y, x = np.mgrid[0:ny, 0:nx].astype(np.float64)
+    z = 2000.0 + 0.3 * x - 0.2 * y + 150.0 * np.sin(x / 17.0) * np.cos(y / 23.0) + 80.0 * np.exp(-((x - nx / 3) ** 2 + (y - ny / 2) ** 2) / 400.0)
+    return z.astype(np.float32).astype(np.float64)
+
+
+def terrain_oracle(dem: np.ndarray, dx: float, dy: float, north=None, south=None):
+    """Horn's 3x3 slope (tan beta) and aspect (downslope direction, radians CCW
+    from east), fp64 numpy: the restatement tfg_terrain_from_dem is checked
+    against.  Rows run north to south; missing halo rows / edge columns
+    replicate the edge."""
+    z = np.asarray(dem, dtype=np.float64)
+    n = z[0] if north is None else np.asarray(north, dtype=np.float64)
+    s_ = z[-1] if south is None else np.asarray(south, dtype=np.float64)
+    p = np.vstack([n[None, :], z, s_[None, :]])
+    p = np.hstack([p[:, :1], p, p[:, -1:]])
+    a, b, c = p[:-2, :-2], p[:-2, 1:-1], p[:-2, 2:]
+    d, f = p[1:-1, :-2], p[1:-1, 2:]
+    g, h, i = p[2:, :-2], p[2:, 1:-1], p[2:, 2:]
+    dzdx = ((c + 2.0 * f + i) - (a + 2.0 * d + g)) * (1.0 / (8.0 * dx))
+    dzds = ((g + 2.0 * h + i) - (a + 2.0 * b + c)) * (1.0 / (8.0 * dy))
+    slope = np.sqrt(dzdx * dzdx + dzds * dzds)
+    aspect = np.where((dzdx == 0) & (dzds == 0), 0.0, np.arctan2(dzds, -dzdx))
+    return slope, aspect
+
+
 def ns(**kw):
     return SimpleNamespace(**kw)

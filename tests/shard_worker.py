@@ -24,7 +24,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["oracle", "gpu"], required=True)
+    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain"], required=True)
     ap.add_argument("--ny", type=int, required=True)
     ap.add_argument("--nx", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
@@ -41,6 +41,31 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     row0, rows = row_block(a.ny, rank, world)
     fields = {}
+    if a.mode in ("halo", "gpu_terrain"):
+        import torch
+
+        from topoflow_glacier.sharding import exchange_halo_rows, terrain_from_dem_sharded
+        from tests.harness import terrain_dem
+
+        dem = terrain_dem(a.ny, a.nx)
+        if a.mode == "halo":
+            block = torch.from_numpy(dem[row0:row0 + rows].copy())
+            north, south = exchange_halo_rows(block[0], block[-1])
+            np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows,
+                     north=np.full(a.nx, np.nan) if north is None else north.numpy(),
+                     south=np.full(a.nx, np.nan) if south is None else south.numpy())
+        else:
+            from tests.harness import BASE_CFG, make_engine
+
+            eng = make_engine(dict(BASE_CFG), rows, a.nx, "float32", n_frames=1, hist_depth=1, row0=row0)
+            eng.set_field("elev", dem[row0:row0 + rows].reshape(-1).astype(np.float32))
+            terrain_from_dem_sharded(eng, 30.0, 30.0)
+            np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, slope=eng.get_field("slope"),
+                     aspect=eng.get_field("aspect"))
+            eng.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     if a.mode == "oracle":
         from tests.harness import oracle_diag, oracle_synthetic
 

@@ -517,6 +517,33 @@ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // ===========================================================================
 // Handle
 // ===========================================================================
+// Horn's 3x3 slope/aspect (tfg_terrain_from_dem).  halo: [2][nx] fp64, the
+// rows north of row 0 and south of row ny-1.  fp64, contraction off, so the
+// numpy restatement in tests reproduces it up to libm rounding.
+template <class R>
+__global__ void k_terrain(const R* __restrict__ elev, const double* __restrict__ halo, R* __restrict__ slope,
+                          R* __restrict__ aspect, int64_t ny, int64_t nx, double inv8dx, double inv8dy) {
+#pragma clang fp contract(off)
+  const int64_t n = ny * nx;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / nx, c = i % nx;
+    const int64_t cw = c > 0 ? c - 1 : c, ce = c < nx - 1 ? c + 1 : c;
+    auto z = [&](int64_t rr, int64_t cc) -> double {
+      if (rr < 0) return halo[cc];
+      if (rr >= ny) return halo[nx + cc];
+      return (double)elev[rr * nx + cc];
+    };
+    const double a = z(r - 1, cw), b = z(r - 1, c), cc_ = z(r - 1, ce);
+    const double d = z(r, cw), f = z(r, ce);
+    const double g = z(r + 1, cw), hh = z(r + 1, c), ii = z(r + 1, ce);
+    const double dzdx = ((cc_ + 2.0 * f + ii) - (a + 2.0 * d + g)) * inv8dx;   // east
+    const double dzds = ((g + 2.0 * hh + ii) - (a + 2.0 * b + cc_)) * inv8dy;  // south
+    slope[i] = (R)sqrt(dzdx * dzdx + dzds * dzds);
+    // downslope direction (-dz/dx, -dz/dnorth) = (-dzdx, +dzds), CCW from east
+    aspect[i] = (R)((dzdx == 0.0 && dzds == 0.0) ? 0.0 : atan2(dzds, -dzdx));
+  }
+}
+
 // Snowfall-window checkpoint I/O (TFG_ST_WINDOW): metres <-> fixed point, and
 // the running total rebuilt from the slots.
 __global__ void k_window_set(int32_t* __restrict__ slot, const double* __restrict__ v, int64_t n, double qscale) {
@@ -571,6 +598,7 @@ struct tfg_handle {
   bool initialised = false;
   bool tot_dirty = false;        // window slots set through TFG_ST_WINDOW
   double* wtmp = nullptr;        // [n_pad] f64 scratch for window I/O
+  double* halo = nullptr;        // [2][nx] f64 DEM halo rows (tfg_terrain_from_dem)
   int64_t last_hist = 0;
   std::string err;
 };
@@ -887,7 +915,7 @@ int tfg_destroy(tfg_handle* h) {
   if (!h) return TFG_OK;
   (void)hipSetDevice(h->device);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
-  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp,
+  void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
@@ -1153,6 +1181,42 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
   h->slope_invalid = false;
   h->geo_dirty = true;
   return tfg_init_state(h);
+}
+
+int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_north, const void* halo_south,
+                         int halo_dtype, int halo_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
+  if (halo_dtype != TFG_F32 && halo_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "halo dtype must be TFG_F32/TFG_F64");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int64_t nx = h->nx, ny = h->ny;
+  if (!h->halo) HIPCHK(h, hipMalloc((void**)&h->halo, (size_t)2 * nx * 8));
+  const size_t rs = h->rsz;
+  const char* el = static_cast<const char*>(h->stat);  // TFG_ST_ELEV plane
+  // a missing halo replicates the shard's own edge row (domain boundary)
+  const void* src[2] = {halo_north, halo_south};
+  for (int k = 0; k < 2; ++k) {
+    if (src[k]) {
+      int rc = upload(h, h->halo + k * nx, TFG_F64, src[k], halo_dtype, nx, halo_on_device);
+      if (rc) return rc;
+    } else {
+      const int64_t row = k == 0 ? 0 : ny - 1;
+      int rc = upload(h, h->halo + k * nx, TFG_F64, el + row * nx * rs, h->engine, nx, 1);
+      if (rc) return rc;
+    }
+  }
+  char* st = static_cast<char*>(h->stat);
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_terrain<float>), grid_for(h->n), 256, 0, h->stream, (const float*)st, h->halo,
+                       (float*)(st + h->n_pad * rs), (float*)(st + 2 * h->n_pad * rs), ny, nx, 1.0 / (8.0 * dx), 1.0 / (8.0 * dy));
+  else
+    hipLaunchKernelGGL((k_terrain<double>), grid_for(h->n), 256, 0, h->stream, (const double*)st, h->halo,
+                       (double*)(st + h->n_pad * rs), (double*)(st + 2 * h->n_pad * rs), ny, nx, 1.0 / (8.0 * dx), 1.0 / (8.0 * dy));
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->geo_dirty = true;
+  h->slope_invalid = false;  // tan(beta) >= 0 always maps into [0, pi/2)
+  return TFG_OK;
 }
 
 const char* tfg_last_error(const tfg_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }

@@ -165,6 +165,31 @@ class GlacierEngine:
         self._chk(self.lib.tfg_get_stream(self.h, ctypes.byref(s)))
         return s.value or 0
 
+    # -- terrain --------------------------------------------------------------------
+    def terrain_from_dem(self, dx: float, dy: float, halo_north=None, halo_south=None) -> None:
+        """Slope/aspect rasters from the elevation raster (Horn 3x3, tfg_terrain_from_dem).
+        Halo rows: numpy arrays or torch CUDA tensors of nx values, None at the domain edge."""
+        ptrs, on_dev, dtype = [], 0, nat.F64
+        keep = []
+        for halo in (halo_north, halo_south):
+            if halo is None:
+                ptrs.append(None)
+                continue
+            if hasattr(halo, "data_ptr") and getattr(halo, "is_cuda", False):
+                t = halo.contiguous().double()
+                keep.append(t)
+                ptrs.append(ctypes.c_void_p(t.data_ptr()))
+                on_dev = 1
+            else:
+                a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(-1))
+                keep.append(a)
+                ptrs.append(a.ctypes.data_as(ctypes.c_void_p))
+            if (keep[-1].numel() if hasattr(keep[-1], "numel") else keep[-1].size) != self.nx:
+                raise ValueError(f"halo rows need nx = {self.nx} values")
+        if on_dev and any(isinstance(k, np.ndarray) for k in keep):
+            raise ValueError("halo rows must be both host arrays or both device tensors")
+        self._chk(self.lib.tfg_terrain_from_dem(self.h, float(dx), float(dy), ptrs[0], ptrs[1], dtype, on_dev))
+
     # -- mass balance -------------------------------------------------------------
     def diagnostics(self) -> np.ndarray:
         """[n_catch][6] = vol_P, vol_PR, vol_PS, vol_SM, vol_IM, P_max of this shard."""

@@ -1,5 +1,10 @@
 """Row-block decomposition of a raster over the GPUs of one node.
 
+The one stencil on the path -- slope/aspect from a DEM (tfg_terrain_from_dem,
+SURVEY.md 8(f) row 4) -- needs the elevation row on each side of a shard: a
+one-row halo exchanged point-to-point between neighbouring ranks
+(:func:`exchange_halo_rows`, RCCL send/recv over xGMI on the GPU path).
+
 Cells are independent in the reference physics (no lateral term: Qc = Qa = 0,
 bmi_topoflow_glacier.py:936-955), so a time step needs no data exchange
 between shards.  The only cross-shard operation is the mass-balance
@@ -12,7 +17,7 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["row_block", "allreduce_diagnostics"]
+__all__ = ["row_block", "allreduce_diagnostics", "exchange_halo_rows", "terrain_from_dem_sharded"]
 
 
 def row_block(ny_global: int, rank: int, world: int) -> tuple[int, int]:
@@ -43,3 +48,45 @@ def allreduce_diagnostics(diag: np.ndarray, group=None, device=None) -> np.ndarr
     out[:, :5] = sums.cpu().numpy()
     out[:, 5] = maxs.cpu().numpy()
     return out
+
+
+def exchange_halo_rows(first_row, last_row, group=None):
+    """(north, south) halo rows of this rank's row block: the last row of rank
+    r-1 and the first row of rank r+1 (None at the domain edges).  first_row /
+    last_row are torch tensors (CUDA for the nccl backend); one batched
+    point-to-point exchange, no collective."""
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return None, None
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    north = torch.empty_like(first_row) if rank > 0 else None
+    south = torch.empty_like(last_row) if rank < world - 1 else None
+    peer = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    ops = []
+    if rank > 0:
+        ops += [dist.P2POp(dist.isend, first_row.contiguous(), peer(rank - 1), group),
+                dist.P2POp(dist.irecv, north, peer(rank - 1), group)]
+    if rank < world - 1:
+        ops += [dist.P2POp(dist.isend, last_row.contiguous(), peer(rank + 1), group),
+                dist.P2POp(dist.irecv, south, peer(rank + 1), group)]
+    for w in dist.batch_isend_irecv(ops):
+        w.wait()
+    return north, south
+
+
+def terrain_from_dem_sharded(eng, dx: float, dy: float, group=None) -> None:
+    """Slope/aspect of a row-block shard (GlacierEngine) with its neighbours'
+    boundary rows as halos: equal to the unsharded result."""
+    import torch
+    import torch.distributed as dist
+
+    elev = eng.get_field("elev").reshape(eng.ny, eng.nx)
+    dev = "cpu"
+    if dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl":
+        dev = f"cuda:{torch.cuda.current_device()}"
+    first = torch.from_numpy(np.ascontiguousarray(elev[0])).to(dev)
+    last = torch.from_numpy(np.ascontiguousarray(elev[-1])).to(dev)
+    north, south = exchange_halo_rows(first, last, group)
+    eng.terrain_from_dem(dx, dy, north, south)
