@@ -24,7 +24,12 @@ Fixtures written (all small .npz, float64):
 * ``dt_quarter.npz`` -- a dt = 0.25 h run; the reference loader rejects float
   dt (config.py:15), so ONLY here the config class is widened to float.
 
+* ``satterlund.npz`` -- SATTERLUND = True (the alternative vapour-pressure and
+  emissivity formulas).
+* ``params.npz`` -- non-default dust_atten / canopy_factor / cloud_factor.
+
 Usage:  python3 tests/golden/make_golden.py   (takes ~1 minute)
+        python3 tests/golden/make_golden.py --only satterlund,params
 """
 
 from __future__ import annotations
@@ -299,6 +304,14 @@ def build_dt(dt, float_dt, nsteps, ncell=8):
     return forc, r, [c["cfg"] for c in cells]
 
 
+def build_variant(extra_cfg, nsteps=288, ncell=8, seed=31):
+    """Perturbed cells under a non-default configuration (SATTERLUND branches
+    :784-796, :1190-1192; dust / canopy / cloud factors config.py:29-31)."""
+    cells, forc = _perturbed_cells(ncell, nsteps, seed, "2013032000", extra_cfg=extra_cfg)
+    r = _run_job({"nsteps": nsteps, "cells": cells})
+    return forc, r, [c["cfg"] for c in cells]
+
+
 def _save(name, forc, r, cfgs, **extra):
     import json
 
@@ -323,7 +336,15 @@ def _save(name, forc, r, cfgs, **extra):
     print("wrote", name, r["outs"].shape)
 
 
-def main():
+def main(only=None):
+    if only:
+        if "satterlund" in only:
+            f, r, c = build_variant({"SATTERLUND": True})
+            _save("satterlund.npz", f, r, c)
+        if "params" in only:
+            f, r, c = build_variant({"dust_atten": 0.14, "canopy_factor": 0.2, "cloud_factor": 0.45}, seed=32)
+            _save("params.npz", f, r, c)
+        return
     f, r, c = build_cat3062920()
     _save("cat3062920_265.npz", f, r, c)
     f, r, c = build_grid64()
@@ -339,5 +360,7 @@ def main():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--child":
         _child_main(sys.argv[2], sys.argv[3])
+    elif len(sys.argv) > 2 and sys.argv[1] == "--only":
+        main(sys.argv[2].split(","))
     else:
         main()

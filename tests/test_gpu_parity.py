@@ -152,7 +152,8 @@ def test_update_until_equals_repeated_update(tmp_path):
 
 
 # ---------------------------------------------------------------- engines vs reference fixtures
-@pytest.mark.parametrize("name", ["grid64", "dt2", "dt_quarter", "clock_dst_end", "clock_dst_start", "clock_new_year"])
+@pytest.mark.parametrize("name", ["grid64", "dt2", "dt_quarter", "clock_dst_end", "clock_dst_start", "clock_new_year",
+                                  "satterlund", "params"])
 def test_fp64_engine_vs_reference_fixtures(name):
     g = load_golden(name)
     n = g["ncell"]
@@ -173,14 +174,15 @@ def test_fp64_engine_vs_reference_fixtures(name):
     assert diag[0, 5] == g["internal"]["P_max"][-1].max()
 
 
-def test_fp32_engine_vs_oracle_on_fixture_inputs():
-    """grid64 inputs rounded to fp32 (as the fp32 engine consumes them), oracle
+@pytest.mark.parametrize("name", ["grid64", "satterlund", "params"])
+def test_fp32_engine_vs_oracle_on_fixture_inputs(name):
+    """Fixture inputs rounded to fp32 (as the fp32 engine consumes them), oracle
     on the identical values; floored tolerance 1e-5."""
-    g = load_golden("grid64")
+    g = load_golden(name)
     r32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
     forcing = {k: r32(v) for k, v in g["forcing"].items()}
     static = {k: r32(v) for k, v in g["static"].items()}
-    outs, state, _ = gpu_run_fields(g["cfg"], static, forcing, 8, 8, "float32", g["nsteps"])
+    outs, state, _ = gpu_run_fields(g["cfg"], static, forcing, 1, g["ncell"], "float32", g["nsteps"])
     ref, _ = oracle_run(g["cfg"], static, forcing)
     flip, genuine = melt_out_flips(outs, ref, 1e-5)
     assert not genuine, genuine

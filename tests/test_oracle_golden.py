@@ -7,7 +7,8 @@ import pytest
 
 from tests.harness import GOLDEN, OUT_NAMES, load_golden, oracle_run
 
-FIXTURES = ["cat3062920_265", "grid64", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter"]
+FIXTURES = ["cat3062920_265", "grid64", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter",
+            "satterlund", "params"]
 RTOL = 1e-12  # bit-exact here; margin for numpy SIMD paths of other host CPUs
 
 
