@@ -100,6 +100,34 @@ __device__ __forceinline__ void vstore(T* __restrict__ base, uint32_t i, const T
   for (int j = 0; j < C; ++j) x.v[j] = v[j];
   *reinterpret_cast<Pack<T, C>*>(reinterpret_cast<char*>(base) + off) = x;
 }
+// Streamed accesses of the step loop: forcing frames and window slots are read
+// once per step and history outputs written once, with far more traffic than
+// the caches hold before any reuse.  TFG_NT_LOAD / TFG_NT_STORE select the
+// non-temporal forms for them (A/B switch).
+#ifndef TFG_NT_LOAD
+#define TFG_NT_LOAD 0
+#endif
+#ifndef TFG_NT_STORE
+#define TFG_NT_STORE 1
+#endif
+template <class T>
+__device__ __forceinline__ T sload(const T* __restrict__ base, uint32_t i) {
+  const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + lane_off(i * (uint32_t)sizeof(T)));
+#if TFG_NT_LOAD
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void sstore(T* __restrict__ base, uint32_t i, T v) {
+  T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + lane_off(i * (uint32_t)sizeof(T)));
+#if TFG_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 template <int C> __device__ __forceinline__ void dload(const double* p, uint32_t i, double (&v)[C]) { vload<double, C>(p, i, v); }
 template <int C> __device__ __forceinline__ void dstore(double* p, uint32_t i, const double (&v)[C]) { vstore<double, C>(p, i, v); }
 template <int C> __device__ __forceinline__ void iload(const int32_t* p, uint32_t i, int32_t (&v)[C]) { vload<int32_t, C>(p, i, v); }
@@ -265,12 +293,13 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
       auto fetch = [&](int k, Frame& f) {
         const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
         const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad;
-        vload<R, C>(fr + F_P * n_pad, lc, f.P);
-        vload<R, C>(fr + F_T * n_pad, lc, f.T);
-        vload<R, C>(fr + F_Q * n_pad, lc, f.Q);
-        vload<R, C>(fr + F_PA * n_pad, lc, f.PA);
-        vload<R, C>(fr + F_UZ * n_pad, lc, f.UZ);
-        iload<C>(ring + (int64_t)un->slot * n_pad, lc, f.q);
+        static_assert(C == 1, "streamed step accesses are per cell");
+        f.P[0] = sload(fr + F_P * n_pad, lc);
+        f.T[0] = sload(fr + F_T * n_pad, lc);
+        f.Q[0] = sload(fr + F_Q * n_pad, lc);
+        f.PA[0] = sload(fr + F_PA * n_pad, lc);
+        f.UZ[0] = sload(fr + F_UZ * n_pad, lc);
+        f.q[0] = sload(ring + (int64_t)un->slot * n_pad, lc);
       };
       auto advance = [&](int k, const Frame& f) {
         const tfg_uniforms* up = uni + k;
@@ -295,14 +324,14 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           }
         }
-        istore<C>(ring + (int64_t)u.slot * n_pad, lc, qn);
+        sstore(ring + (int64_t)u.slot * n_pad, lc, qn[0]);
         R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad;
-        vstore<R, C>(h + H_HSNOW * n_pad, lc, o_hs);
-        vstore<R, C>(h + H_SM * n_pad, lc, o_sm);
-        vstore<R, C>(h + H_HICE * n_pad, lc, o_hi);
-        vstore<R, C>(h + H_IM * n_pad, lc, o_im);
-        vstore<R, C>(h + H_MTOT * n_pad, lc, o_mt);
-        vstore<R, C>(h + H_RH * n_pad, lc, o_rh);
+        sstore(h + H_HSNOW * n_pad, lc, o_hs[0]);
+        sstore(h + H_SM * n_pad, lc, o_sm[0]);
+        sstore(h + H_HICE * n_pad, lc, o_hi[0]);
+        sstore(h + H_IM * n_pad, lc, o_im[0]);
+        sstore(h + H_MTOT * n_pad, lc, o_mt[0]);
+        sstore(h + H_RH * n_pad, lc, o_rh[0]);
       };
 #if TFG_PREFETCH_DEPTH == 2
       Frame fa, fb, fc;
