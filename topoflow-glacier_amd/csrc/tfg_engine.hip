@@ -110,9 +110,11 @@ __device__ __forceinline__ void vstore(T* __restrict__ base, uint32_t i, const T
 #ifndef TFG_NT_STORE
 #define TFG_NT_STORE 1
 #endif
+// `off` is the lane's byte offset, materialised once per basic block by the
+// caller (lane_off), shared by every access of that block.
 template <class T>
-__device__ __forceinline__ T sload(const T* __restrict__ base, uint32_t i) {
-  const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + lane_off(i * (uint32_t)sizeof(T)));
+__device__ __forceinline__ T sload(const T* __restrict__ base, uint32_t off) {
+  const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
 #if TFG_NT_LOAD
   return __builtin_nontemporal_load(p);
 #else
@@ -120,8 +122,8 @@ __device__ __forceinline__ T sload(const T* __restrict__ base, uint32_t i) {
 #endif
 }
 template <class T>
-__device__ __forceinline__ void sstore(T* __restrict__ base, uint32_t i, T v) {
-  T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + lane_off(i * (uint32_t)sizeof(T)));
+__device__ __forceinline__ void sstore(T* __restrict__ base, uint32_t off, T v) {
+  T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
 #if TFG_NT_STORE
   __builtin_nontemporal_store(v, p);
 #else
@@ -294,12 +296,14 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
         const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
         const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad;
         static_assert(C == 1, "streamed step accesses are per cell");
-        f.P[0] = sload(fr + F_P * n_pad, lc);
-        f.T[0] = sload(fr + F_T * n_pad, lc);
-        f.Q[0] = sload(fr + F_Q * n_pad, lc);
-        f.PA[0] = sload(fr + F_PA * n_pad, lc);
-        f.UZ[0] = sload(fr + F_UZ * n_pad, lc);
-        f.q[0] = sload(ring + (int64_t)un->slot * n_pad, lc);
+        static_assert(sizeof(R) == 4 || sizeof(R) == 8, "R is float or double");
+        const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
+        f.P[0] = sload(fr + F_P * n_pad, oR);
+        f.T[0] = sload(fr + F_T * n_pad, oR);
+        f.Q[0] = sload(fr + F_Q * n_pad, oR);
+        f.PA[0] = sload(fr + F_PA * n_pad, oR);
+        f.UZ[0] = sload(fr + F_UZ * n_pad, oR);
+        f.q[0] = sload(ring + (int64_t)un->slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u));
       };
       auto advance = [&](int k, const Frame& f) {
         const tfg_uniforms* up = uni + k;
@@ -324,14 +328,15 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           }
         }
-        sstore(ring + (int64_t)u.slot * n_pad, lc, qn[0]);
+        const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
+        sstore(ring + (int64_t)u.slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u), qn[0]);
         R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad;
-        sstore(h + H_HSNOW * n_pad, lc, o_hs[0]);
-        sstore(h + H_SM * n_pad, lc, o_sm[0]);
-        sstore(h + H_HICE * n_pad, lc, o_hi[0]);
-        sstore(h + H_IM * n_pad, lc, o_im[0]);
-        sstore(h + H_MTOT * n_pad, lc, o_mt[0]);
-        sstore(h + H_RH * n_pad, lc, o_rh[0]);
+        sstore(h + H_HSNOW * n_pad, oR, o_hs[0]);
+        sstore(h + H_SM * n_pad, oR, o_sm[0]);
+        sstore(h + H_HICE * n_pad, oR, o_hi[0]);
+        sstore(h + H_IM * n_pad, oR, o_im[0]);
+        sstore(h + H_MTOT * n_pad, oR, o_mt[0]);
+        sstore(h + H_RH * n_pad, oR, o_rh[0]);
       };
 #if TFG_PREFETCH_DEPTH == 2
       Frame fa, fb, fc;

@@ -601,13 +601,15 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
   float albedo;
   {
+    // selects in fp32: albedo is rebuilt every step from n and the depths
+    // (the previous value survives only for a NaN snow depth)
     const float r = (T_air > 0.0f) ? (0.12f * kLog2e) : (0.05f * kLog2e);
     const float snow_albedo = 0.4f + 0.44f * fexp2(-(float)st.n * r);
-    double a = snow_pos ? (double)snow_albedo : st.albedo;
-    if (st.h_snow == 0.0 && ice_pos) a = 0.3;
-    if (st.h_snow == 0.0 && st.h_ice == 0.0) a = 0.15;
-    st.albedo = a;
-    albedo = (float)a;
+    float a = snow_pos ? snow_albedo : (float)st.albedo;
+    if (st.h_snow == 0.0 && ice_pos) a = 0.3f;
+    if (st.h_snow == 0.0 && st.h_ice == 0.0) a = 0.15f;
+    st.albedo = (double)a;
+    albedo = a;
   }
   // clear-sky shortwave (SF:904-941); W_p = 1.12*w
   const float w = fexp2((0.0614f * kLog2e) * T_dew);
