@@ -153,9 +153,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal switches for a one-GPU box (not used by the driver): every rank on
+    # cuda:0 and gloo for the barrier / max-over-ranks / diagnostics reductions.
+    backend = os.environ.get("TFG_BENCH_BACKEND", "nccl")
+    if os.environ.get("TFG_BENCH_ONE_DEVICE") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     if args.scaling == "weak":
         ny_global = args.ny * world
         row0, rows = rank * args.ny, args.ny
@@ -193,7 +201,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
