@@ -6,7 +6,7 @@
 // + six outputs).  Reports GB/s for several (R, W) mixes so the measured
 // k_fused rate can be placed against what this read/write mix can reach.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
-//   tools/hbm_mix [cells=67108864] [steps=24]
+//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048]
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -25,8 +25,8 @@ __device__ __forceinline__ void splat(float& o, float a) { o = a; }
 __device__ __forceinline__ void splat(float2& o, float a) { o = make_float2(a, a + 1.0f); }
 __device__ __forceinline__ void splat(float4& o, float a) { o = make_float4(a, a + 1.0f, a + 2.0f, a + 3.0f); }
 
-// V floats (V adjacent cells) per lane per plane
-template <int R, int W, int V>
+// V floats (V adjacent cells) per lane per plane; NT: non-temporal stores
+template <int R, int W, int V, bool NT = false>
 __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
                                              int steps, int frames) {
   using T = typename Vec<V>::T;
@@ -43,25 +43,32 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float
       for (int r = 0; r < R; ++r) acc += hsum(v[r]);
       T* fo = reinterpret_cast<T*>(out + (size_t)(s % frames) * W * n);
 #pragma unroll
-      for (int w = 0; w < W; ++w) { T o; splat(o, acc + (float)w); fo[(size_t)w * nv + i] = o; }
+      for (int w = 0; w < W; ++w) {
+        T o;
+        splat(o, acc + (float)w);
+        if constexpr (NT) __builtin_nontemporal_store(o, &fo[(size_t)w * nv + i]);
+        else fo[(size_t)w * nv + i] = o;
+      }
     }
     if (W == 0 && acc == -1.0f) out[i] = acc;  // keep the reads alive
   }
 }
 
-template <int R, int W, int V = 1>
+static int g_blocks = 256 * 8;
+
+template <int R, int W, int V = 1, bool NT = false>
 void run(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
-  const int blocks = 256 * 8;
-  k_mix<R, W, V><<<blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  const int blocks = g_blocks;
+  k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames);  // warm-up
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
     CHECK(hipEventRecord(a));
-    k_mix<R, W, V><<<blocks, 256>>>(in, out, n, steps, frames);
+    k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms;
@@ -69,8 +76,8 @@ void run(const char* name, float* in, float* out, uint32_t n, int steps, int fra
     if (ms < best) best = ms;
   }
   const double bytes = (double)n * steps * 4.0 * (R + W);
-  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"bytes_per_lane\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
-              name, R, W, 4 * V, bytes / (best * 1e-3) / 1e9, best);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"bytes_per_lane\": %d, \"blocks\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, 4 * V, g_blocks, bytes / (best * 1e-3) / 1e9, best);
   CHECK(hipEventDestroy(a));
   CHECK(hipEventDestroy(b));
 }
@@ -78,6 +85,7 @@ void run(const char* name, float* in, float* out, uint32_t n, int steps, int fra
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
+  if (argc > 3) g_blocks = std::atoi(argv[3]);
   const int frames = steps;  // one distinct frame per step, as k_fused (no address is touched twice)
   float *in, *out;
   CHECK(hipMalloc(&in, (size_t)n * 4 * 7 * frames));
@@ -85,6 +93,7 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(in, 0, (size_t)n * 4 * 7 * frames));
   CHECK(hipMemset(out, 0, (size_t)n * 4 * 7 * frames));
   run<6, 7>("k_fused step mix (6 read, 7 write)", in, out, n, steps, frames);
+  run<6, 7, 1, true>("k_fused step mix, non-temporal stores", in, out, n, steps, frames);
   run<7, 0>("read only (7 planes)", in, out, n, steps, frames);
   run<0, 7>("write only (7 planes)", in, out, n, steps, frames);
   run<1, 1>("copy (1 read, 1 write)", in, out, n, steps, frames);
