@@ -430,3 +430,28 @@ def test_fp32_free_run_over_a_year(oracle_year):
     assert frac_cells("h_ice")[1] <= 0.05, frac_cells("h_ice")
     rel = np.abs(diag - Y["diag"]) / np.abs(Y["diag"])
     assert np.all(rel[[0, 1, 2, 5]] <= 1e-8) and rel[3] <= 1e-5 and rel[4] <= 1e-4, rel
+
+
+def test_fp64_engine_propagates_nan_forcing_like_the_reference():
+    """Missing forcing (NaN) takes the same path as in the reference's numpy
+    arithmetic: np.maximum / np.minimum propagate NaN (:1364-1434), a NaN
+    snowfall poisons the window sum (:1040), so outputs turn NaN in the same
+    cells and steps and finite values still match.  (The fp32 engine uses IEEE
+    min/max and does not model missing data)"""
+    g = load_golden("grid64")
+    cells = slice(8, 16)
+    forcing = {k: np.array(v[:40, cells], copy=True) for k, v in g["forcing"].items()}
+    static = {k: v[cells] for k, v in g["static"].items()}
+    forcing["T_air"][3, 0] = np.nan
+    forcing["P"][5, 1] = np.nan
+    forcing["Hum_sp"][2, 2] = np.nan
+    forcing["uz"][7, 3] = np.nan
+    forcing["P_air"][9, 4] = np.nan
+    outs, state, diag = gpu_run_fields(g["cfg"], static, forcing, 1, 8, "float64", 40)
+    ref, m = oracle_run(g["cfg"], static, forcing)
+    for v in HIST:
+        np.testing.assert_array_equal(np.isnan(outs[v]), np.isnan(ref[v]), err_msg=v)
+        ok = ~np.isnan(ref[v])
+        assert _rel(outs[v][ok], ref[v][ok]) <= 1e-10, v
+    assert np.isnan(ref["M_total"][-1, :5]).all() and np.isfinite(ref["M_total"][-1, 5:]).all()
+    np.testing.assert_array_equal(np.isnan(diag[0, :5]), np.isnan([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM]))

@@ -191,3 +191,22 @@ def test_synthetic_mirror_is_deterministic_and_in_range():
     assert 0.2 < frac < 0.28
     u = hash_u01(1, 0, 0, np.arange(100000))
     assert 0.0 <= u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
+
+
+def test_create_rejects_oversize_shards_before_touching_the_gpu():
+    """32-bit lane offsets (tfg.h): ny*nx*8 must stay below 2^32; the check runs
+    before any HIP call, so it holds without a device."""
+    import ctypes
+
+    from topoflow_glacier import _native as nat
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import params_from_config
+
+    L = nat.load()
+    p = params_from_config(TopoflowGlacierConfig.model_validate(dict(BASE_CFG)))
+    h = ctypes.c_void_p()
+    rc = L.tfg_create(ctypes.byref(p), 32768, 16384, nat.F32, 0, 1, 1, 1, ctypes.byref(h))
+    assert rc == nat.ERR_ARG and b"too large" in L.tfg_last_error(None)
+    for bad in ((0, 8, nat.F32, 1, 1, 1), (8, 8, 7, 1, 1, 1), (8, 8, nat.F32, 0, 1, 1), (8, 8, nat.F32, 1, 1, 513)):
+        ny, nx, eng, fr, hd, nc = bad
+        assert L.tfg_create(ctypes.byref(p), ny, nx, eng, 0, fr, hd, nc, ctypes.byref(h)) == nat.ERR_ARG, bad
