@@ -175,6 +175,20 @@ int tfg_get_stream(tfg_handle* h, void** stream);
 int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_dtype,
                   int64_t n, int src_on_device);
 
+/* The five inputs the physics reads, for one forcing frame, in one call:
+ * src is [5][n] in _dynamic_input_vars order without the radiation terms
+ * (bmi_topoflow_glacier.py:18-26): P_air, Hum_sp, P, T_air, uz.  Host data is
+ * copied into a pinned staging ring, so the call returns without waiting for
+ * the device.  Replaces: the per-step set_value() calls of a caller
+ * (examples/run_topoflow_glacier.py:63-71). */
+int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int64_t n, int src_on_device);
+
+/* The eight BMI outputs in _output_vars order (:28-37): h_snow, h_swe, SM,
+ * h_ice, h_iwe, IM, M_total, RH, as dst[8][n], from output-history slot
+ * `hist` (h_swe/h_iwe: the current state).  One gather and one copy.
+ * Replaces: the per-step get_value() calls (:1810-1822). */
+int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n, int dst_on_device);
+
 /* Copy n cells of a field out.  `index` is the history slot for TFG_OUT_*
  * (except H_SWE/H_IWE, which are state), the frame for TFG_IN_*.
  * Replaces: get_value / get_value_ptr (:1810-1828). */

@@ -1,0 +1,40 @@
+"""Per-step latency of the single-catchment BMI path (set_value x7, update,
+get_value x8), as NextGen drives it.  Diagnostic."""
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import yaml
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
+from tests.harness import BASE_CFG, GOLDEN  # noqa: E402
+from topoflow_glacier import BmiTopoflowGlacier  # noqa: E402
+from topoflow_glacier.forcing import read_forcing_csv  # noqa: E402
+from topoflow_glacier.run import OUT_BMI  # noqa: E402
+
+cfg = Path("/tmp/bmi_lat.yaml")
+cfg.write_text(yaml.dump(BASE_CFG))
+t = read_forcing_csv(GOLDEN / "sample-cat-3062920.csv", BASE_CFG["start_time"], BASE_CFG["end_time"])
+for rep in range(3):
+    m = BmiTopoflowGlacier()
+    t0 = time.perf_counter()
+    m.initialize(cfg)
+    t1 = time.perf_counter()
+    d = np.zeros(1)
+    ts, tu, tg = 0.0, 0.0, 0.0
+    for i in range(len(t)):
+        a = time.perf_counter()
+        t.apply(m, i)
+        b = time.perf_counter()
+        m.update()
+        c = time.perf_counter()
+        for name in OUT_BMI.values():
+            m.get_value(name, d)
+        e = time.perf_counter()
+        ts, tu, tg = ts + b - a, tu + c - b, tg + e - c
+    m.finalize()
+    n = len(t)
+    print(f"rep {rep}: initialize {1e3 * (t1 - t0):.1f} ms; per step: set_value x7 {1e6 * ts / n:.1f} us, "
+          f"update {1e6 * tu / n:.1f} us, get_value x8 {1e6 * tg / n:.1f} us, total {1e6 * (ts + tu + tg) / n:.1f} us", flush=True)

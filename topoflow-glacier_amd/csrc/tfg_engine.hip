@@ -582,6 +582,32 @@ __global__ void k_terrain(const R* __restrict__ elev, const double* __restrict__
   }
 }
 
+// tfg_set_inputs / tfg_get_outputs: the per-step BMI traffic of one call each.
+// src [5][n]: P_air, Hum_sp, P, T_air, uz (BMI order) -> frame planes.
+template <class R, class S>
+__global__ void k_scatter_inputs(R* __restrict__ fr, const S* __restrict__ src, int64_t n, int64_t n_pad) {
+  const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll
+    for (int f = 0; f < 5; ++f) fr[map[f] * n_pad + i] = (R)src[f * n + i];
+}
+// dst [8][n]: h_snow, h_swe, SM, h_ice, h_iwe, IM, M_total, RH.  Before the
+// first step (depths not yet derived) the depths come from the fp64 state.
+template <class R, class D>
+__global__ void k_gather_outputs(D* __restrict__ dst, const R* __restrict__ hs, const double* __restrict__ st, int64_t n,
+                                 int64_t n_pad, int depths_from_state) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    dst[0 * n + i] = depths_from_state ? (D)st[S_HSNOW * n_pad + i] : (D)hs[H_HSNOW * n_pad + i];
+    dst[1 * n + i] = (D)st[S_HSWE * n_pad + i];
+    dst[2 * n + i] = (D)hs[H_SM * n_pad + i];
+    dst[3 * n + i] = depths_from_state ? (D)st[S_HICE * n_pad + i] : (D)hs[H_HICE * n_pad + i];
+    dst[4 * n + i] = (D)st[S_HIWE * n_pad + i];
+    dst[5 * n + i] = (D)hs[H_IM * n_pad + i];
+    dst[6 * n + i] = (D)hs[H_MTOT * n_pad + i];
+    dst[7 * n + i] = (D)hs[H_RH * n_pad + i];
+  }
+}
+
 // Snowfall-window checkpoint I/O (TFG_ST_WINDOW): metres <-> fixed point, and
 // the running total rebuilt from the slots.
 __global__ void k_window_set(int32_t* __restrict__ slot, const double* __restrict__ v, int64_t n, double qscale) {
@@ -637,6 +663,16 @@ struct tfg_handle {
   bool tot_dirty = false;        // window slots set through TFG_ST_WINDOW
   double* wtmp = nullptr;        // [n_pad] f64 scratch for window I/O
   double* halo = nullptr;        // [2][nx] f64 DEM halo rows (tfg_terrain_from_dem)
+  // tfg_set_inputs: pinned host staging ring (2 slots) + device staging
+  void* in_h[2] = {nullptr, nullptr};
+  void* in_d[2] = {nullptr, nullptr};
+  size_t in_cap[2] = {0, 0};
+  hipEvent_t in_ev[2] = {nullptr, nullptr};
+  int in_next = 0;
+  // tfg_get_outputs: device gather buffer + pinned host buffer
+  void* out_d = nullptr;
+  void* out_h = nullptr;
+  size_t out_cap = 0;
   int64_t last_hist = 0;
   std::string err;
 };
@@ -968,7 +1004,12 @@ int tfg_destroy(tfg_handle* h) {
   for (int i = 0; i < 2; ++i) {
     if (h->h_u[i]) (void)hipHostFree(h->h_u[i]);
     if (h->h_u_ev[i]) (void)hipEventDestroy(h->h_u_ev[i]);
+    if (h->in_h[i]) (void)hipHostFree(h->in_h[i]);
+    if (h->in_d[i]) (void)hipFree(h->in_d[i]);
+    if (h->in_ev[i]) (void)hipEventDestroy(h->in_ev[i]);
   }
+  if (h->out_d) (void)hipFree(h->out_d);
+  if (h->out_h) (void)hipHostFree(h->out_h);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return TFG_OK;
@@ -1228,6 +1269,92 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
   h->slope_invalid = false;
   h->geo_dirty = true;
   return tfg_init_state(h);
+}
+
+int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int64_t n, int src_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!src) return fail(h, TFG_ERR_ARG, "null src");
+  if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
+  if (frame < 0 || frame >= h->n_frames) return fail(h, TFG_ERR_ARG, "frame index out of range");
+  if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t bytes = (size_t)5 * n * dtype_size(src_dtype);
+  const void* dsrc = src;
+  int b = -1;
+  if (!src_on_device) {
+    // the host buffer is borrowed for this call only: copy it into a pinned
+    // slot whose previous transfer has completed, then transfer asynchronously
+    b = h->in_next;
+    h->in_next ^= 1;
+    if (h->in_ev[b]) HIPCHK(h, hipEventSynchronize(h->in_ev[b]));
+    else HIPCHK(h, hipEventCreateWithFlags(&h->in_ev[b], hipEventDisableTiming));
+    if (h->in_cap[b] < bytes) {
+      if (h->in_h[b]) HIPCHK(h, hipHostFree(h->in_h[b]));
+      if (h->in_d[b]) HIPCHK(h, hipFree(h->in_d[b]));
+      h->in_h[b] = h->in_d[b] = nullptr;
+      h->in_cap[b] = 0;
+      HIPCHK(h, hipHostMalloc(&h->in_h[b], bytes, hipHostMallocDefault));
+      HIPCHK(h, hipMalloc(&h->in_d[b], bytes));
+      h->in_cap[b] = bytes;
+    }
+    std::memcpy(h->in_h[b], src, bytes);
+    HIPCHK(h, hipMemcpyAsync(h->in_d[b], h->in_h[b], bytes, hipMemcpyHostToDevice, h->stream));
+    dsrc = h->in_d[b];
+  }
+  char* fr = static_cast<char*>(h->forc) + (size_t)frame * kNumForc * h->n_pad * h->rsz;
+  const int gb = grid_for(n);
+  if (h->engine == TFG_F32 && src_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_scatter_inputs<float, float>), gb, 256, 0, h->stream, (float*)fr, (const float*)dsrc, n, h->n_pad);
+  else if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_scatter_inputs<float, double>), gb, 256, 0, h->stream, (float*)fr, (const double*)dsrc, n, h->n_pad);
+  else if (src_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_scatter_inputs<double, float>), gb, 256, 0, h->stream, (double*)fr, (const float*)dsrc, n, h->n_pad);
+  else
+    hipLaunchKernelGGL((k_scatter_inputs<double, double>), gb, 256, 0, h->stream, (double*)fr, (const double*)dsrc, n, h->n_pad);
+  HIPCHK(h, hipGetLastError());
+  if (b >= 0) HIPCHK(h, hipEventRecord(h->in_ev[b], h->stream));
+  return TFG_OK;
+}
+
+int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
+  if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
+  if (hist < 0 || hist >= h->hist_depth) return fail(h, TFG_ERR_ARG, "history slot out of range");
+  if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+  HIPCHK(h, hipSetDevice(h->device));
+  const size_t bytes = (size_t)8 * n * dtype_size(dst_dtype);
+  void* gdst = dst;
+  if (!dst_on_device) {
+    if (h->out_cap < bytes) {
+      if (h->out_d) HIPCHK(h, hipFree(h->out_d));
+      if (h->out_h) HIPCHK(h, hipHostFree(h->out_h));
+      h->out_d = h->out_h = nullptr;
+      h->out_cap = 0;
+      HIPCHK(h, hipMalloc(&h->out_d, bytes));
+      HIPCHK(h, hipHostMalloc(&h->out_h, bytes, hipHostMallocDefault));
+      h->out_cap = bytes;
+    }
+    gdst = h->out_d;
+  }
+  const char* hs = static_cast<const char*>(h->hist) + (size_t)hist * kNumHist * h->n_pad * h->rsz;
+  const int from_state = h->depths_derived ? 0 : 1;
+  const int gb = grid_for(n);
+  if (h->engine == TFG_F32 && dst_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<float, float>), gb, 256, 0, h->stream, (float*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
+  else if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<float, double>), gb, 256, 0, h->stream, (double*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
+  else if (dst_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<double, float>), gb, 256, 0, h->stream, (float*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
+  else
+    hipLaunchKernelGGL((k_gather_outputs<double, double>), gb, 256, 0, h->stream, (double*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
+  HIPCHK(h, hipGetLastError());
+  if (!dst_on_device) {
+    HIPCHK(h, hipMemcpyAsync(h->out_h, h->out_d, bytes, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::memcpy(dst, h->out_h, bytes);
+  }
+  return TFG_OK;
 }
 
 int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_north, const void* halo_south,

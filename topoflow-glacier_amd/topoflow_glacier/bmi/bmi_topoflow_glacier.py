@@ -76,6 +76,7 @@ INTERNAL_NAME_CROSSWALK = {
 }
 EXTERNAL_NAME_CROSSWALK = {v: k for k, v in INTERNAL_NAME_CROSSWALK.items()}
 _PHYSICS_INPUTS = ("P", "T_air", "Hum_sp", "P_air", "uz")  # LW_in / SW_in are never read (:1122, :1235)
+_INPUT_BLOCK = ("P_air", "Hum_sp", "P", "T_air", "uz")  # tfg_set_inputs order
 _EAGER_MAX_CELLS = 4096
 
 
@@ -201,6 +202,8 @@ class BmiTopoflowGlacier(BmiBase):
         self._dynamic_inputs = build_context(_dynamic_input_vars, n)
         self._outputs = build_context(_output_vars, n)
         self._eager = n <= _EAGER_MAX_CELLS
+        self._in_block = np.empty((5, n), dtype=np.float64)
+        self._out_block = np.empty((8, n), dtype=np.float64)
         self._engine = make_engine(cfg)
         self._beta_invalid = configure_engine(self._engine, cfg)
         for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
@@ -229,8 +232,11 @@ class BmiTopoflowGlacier(BmiBase):
 
     def _push_inputs(self) -> None:
         eng = self._engine
-        for name in _PHYSICS_INPUTS:
-            eng.set_field(name, self._dynamic_inputs.value(_ext(name)))
+        n = self.n_cells
+        block = self._in_block
+        for i, name in enumerate(_INPUT_BLOCK):  # one transfer for the five inputs (tfg_set_inputs)
+            block[i] = np.broadcast_to(self._dynamic_inputs.value(_ext(name)), (n,))
+        eng.set_inputs(block, 0)
         for name in sorted(self._dirty_outputs):
             eng.set_field(name, self._outputs.value(_ext(name)))
         self._dirty_outputs.clear()
@@ -243,8 +249,7 @@ class BmiTopoflowGlacier(BmiBase):
         self._timestep += nsteps
         self._stale = {_int(n) for n, _ in _output_vars}
         if self._eager:
-            for name in list(self._stale):
-                self._refresh(name)
+            self._refresh_all()
 
     def update(self) -> None:
         """Advance one time step (reference :413-465) on the GPU."""
@@ -278,6 +283,13 @@ class BmiTopoflowGlacier(BmiBase):
             self._engine = None
 
     # ------------------------------------------------------------- mirrors
+    def _refresh_all(self) -> None:
+        """All eight outputs in one gather + copy (tfg_get_outputs)."""
+        out = self._engine.get_outputs(out=self._out_block)
+        for j, (name, _) in enumerate(_output_vars):
+            self._outputs.value(name)[:] = out[j]
+        self._stale.clear()
+
     def _refresh(self, internal: str) -> None:
         ext = _ext(internal)
         self._outputs.value(ext)[:] = self._engine.get_field(internal)

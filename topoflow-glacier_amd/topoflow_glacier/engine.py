@@ -119,6 +119,23 @@ class GlacierEngine:
         self._chk(self.lib.tfg_get_field(self.h, fid, index, out.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
         return out
 
+    def set_inputs(self, values: np.ndarray, index: int = 0) -> None:
+        """The five physics inputs of one frame in one call: values [5][n] in
+        BMI order P_air, Hum_sp, P, T_air, uz (tfg_set_inputs)."""
+        a = np.ascontiguousarray(values, dtype=np.float64)
+        if a.shape != (5, self.n):
+            raise ValueError(f"inputs must be [5][{self.n}]")
+        self._chk(self.lib.tfg_set_inputs(self.h, int(index), a.ctypes.data_as(ctypes.c_void_p), nat.F64, self.n, 0))
+
+    def get_outputs(self, index: int | None = None, out: np.ndarray | None = None) -> np.ndarray:
+        """The eight BMI outputs [8][n] (h_snow, h_swe, SM, h_ice, h_iwe, IM,
+        M_total, RH) of history slot `index` (default: the newest) in one call."""
+        if out is None:
+            out = np.empty((8, self.n), dtype=np.float64)
+        idx = self.last_hist if index is None else int(index)
+        self._chk(self.lib.tfg_get_outputs(self.h, idx, out.ctypes.data_as(ctypes.c_void_p), nat.F64, self.n, 0))
+        return out
+
     @property
     def last_hist(self) -> int:
         return (self.step_index - 1) % self.hist_depth if self.step_index > 0 else 0
@@ -135,11 +152,23 @@ class GlacierEngine:
         self.step_index = 0
 
     # -- time stepping ------------------------------------------------------------
+    _UBLOCK = 512  # steps of uniforms computed at once for short runs
+
     def uniforms(self, nsteps: int, frames=None) -> np.ndarray:
         k0 = self.step_index
         hist = (np.arange(k0, k0 + nsteps) % self.hist_depth).astype(np.int32)
         if frames is None:
             frames = (np.arange(k0, k0 + nsteps) % self.n_frames).astype(np.int32)
+        b0 = k0 - k0 % self._UBLOCK
+        if nsteps <= self._UBLOCK and k0 + nsteps <= b0 + self._UBLOCK:
+            # per-step callers (BMI update()): serve from a block computed once
+            cache = getattr(self, "_ucache", None)
+            if cache is None or cache[0] != b0:
+                cache = (b0, self.clock.uniforms(b0, self._UBLOCK))
+                self._ucache = cache
+            u = cache[1][k0 - b0:k0 - b0 + nsteps].copy()
+            u["frame"], u["hist"] = frames, hist
+            return u
         return self.clock.uniforms(k0, nsteps, frames=frames, hist=hist)
 
     def run(self, nsteps: int = 1, uniforms: np.ndarray | None = None, frames=None) -> None:

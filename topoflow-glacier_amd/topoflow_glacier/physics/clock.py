@@ -113,7 +113,20 @@ class StepClock:
     # -- calendar ----------------------------------------------------------
     def calendar(self, k0: int, n: int):
         """(julian_day, year, GMT_offset, TSN_offset) for steps k0..k0+n-1
-        (update_julian_day :957-1004)."""
+        (update_julian_day :957-1004).  Short requests are served from blocks
+        of 512 steps computed once."""
+        B = 512
+        b0 = k0 - k0 % B
+        if n <= B and k0 + n <= b0 + B:
+            cache = getattr(self, "_cal_cache", None)
+            if cache is None or cache[0] != b0:
+                cache = (b0, self._calendar(b0, B))
+                self._cal_cache = cache
+            i = k0 - b0
+            return tuple(a[i:i + n] for a in cache[1])
+        return self._calendar(k0, n)
+
+    def _calendar(self, k0: int, n: int):
         jd = np.empty(n)
         yr = np.empty(n, dtype=np.int64)
         gmt = np.empty(n)
