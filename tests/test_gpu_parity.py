@@ -455,3 +455,34 @@ def test_fp64_engine_propagates_nan_forcing_like_the_reference():
         assert _rel(outs[v][ok], ref[v][ok]) <= 1e-10, v
     assert np.isnan(ref["M_total"][-1, :5]).all() and np.isfinite(ref["M_total"][-1, 5:]).all()
     np.testing.assert_array_equal(np.isnan(diag[0, :5]), np.isnan([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM]))
+
+
+@pytest.mark.parametrize("engine", ["float32", "float64"])
+def test_batched_io_equals_per_field_io(engine):
+    """tfg_set_inputs == five tfg_set_field calls; tfg_get_outputs == the
+    eight tfg_get_field reads (BMI order), on a padded grid (5 x 13 cells)."""
+    ny, nx, n = 5, 13, 65
+    syn, d = synthetic_inputs(21, ny, nx, 24)
+    names = ("P_air", "Hum_sp", "P", "T_air", "uz")
+    outs = []
+    for batched in (False, True):
+        e = make_engine(BASE_CFG, ny, nx, engine, n_frames=1, hist_depth=2)
+        try:
+            e.fill_synthetic(21, d)
+            for k in range(6):
+                vals = np.stack([syn[v][k].astype(np.float64) for v in names])
+                if batched:
+                    e.set_inputs(vals, 0)
+                else:
+                    for v, x in zip(names, vals):
+                        e.set_field(v, x, index=0)
+                e.run(1, frames=np.zeros(1, dtype=np.int32))
+            if batched:
+                got = e.get_outputs()
+            else:
+                got = np.stack([e.get_field(v) for v in ("h_snow", "h_swe", "SM", "h_ice", "h_iwe", "IM", "M_total", "RH")])
+            outs.append(got)
+        finally:
+            e.close()
+    assert outs[0].shape == (8, n)
+    np.testing.assert_array_equal(outs[0], outs[1])
