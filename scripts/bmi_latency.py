@@ -38,3 +38,34 @@ for rep in range(3):
     n = len(t)
     print(f"rep {rep}: initialize {1e3 * (t1 - t0):.1f} ms; per step: set_value x7 {1e6 * ts / n:.1f} us, "
           f"update {1e6 * tu / n:.1f} us, get_value x8 {1e6 * tg / n:.1f} us, total {1e6 * (ts + tu + tg) / n:.1f} us", flush=True)
+
+# breakdown of update(): Python side vs the three native calls
+from topoflow_glacier import engine as E  # noqa: E402
+
+acc = {}
+
+
+def timed(name, fn):
+    def w(*a, **k):
+        t0 = time.perf_counter()
+        r = fn(*a, **k)
+        acc[name] = acc.get(name, 0.0) + time.perf_counter() - t0
+        return r
+    return w
+
+
+E.GlacierEngine.set_inputs = timed("set_inputs", E.GlacierEngine.set_inputs)
+E.GlacierEngine.run = timed("run (uniforms + tfg_step)", E.GlacierEngine.run)
+E.GlacierEngine.uniforms = timed("  uniforms (Python)", E.GlacierEngine.uniforms)
+E.GlacierEngine.get_outputs = timed("get_outputs", E.GlacierEngine.get_outputs)
+m = BmiTopoflowGlacier()
+m.initialize(cfg)
+t0 = time.perf_counter()
+for i in range(len(t)):
+    t.apply(m, i)
+    m.update()
+tot = time.perf_counter() - t0
+m.finalize()
+n = len(t)
+print(f"breakdown per step (us): total incl. set_value {1e6 * tot / n:.1f}; " +
+      "; ".join(f"{k} {1e6 * v / n:.1f}" for k, v in acc.items()), flush=True)

@@ -39,7 +39,10 @@ using tfg::CellStatic;
 using tfg::CellStaticF;
 using tfg::DevParams;
 
-constexpr int kBlock = 256;
+#ifndef TFG_BLOCK
+#define TFG_BLOCK 256
+#endif
+constexpr int kBlock = TFG_BLOCK;  // threads per workgroup
 #ifndef TFG_CELLS_PER_THREAD
 #define TFG_CELLS_PER_THREAD 1
 #endif
