@@ -13,7 +13,8 @@
 //
 // Mass-balance diagnostics (vol_P/PR/PS/SM/IM, P_max: :558-624, :1482-1494)
 // are reduced without atomics: lane registers -> wave butterfly (__shfl_xor) ->
-// per-wave LDS bins -> one slab row per workgroup -> k_diag_reduce, which folds
+// per-wave LDS bins -> one slab row per workgroup (accumulated over launches)
+// -> k_diag_reduce when the diagnostics are read, which folds
 // the slab into the running fp64 totals in a fixed order (bitwise
 // reproducible).
 #include <hip/hip_runtime.h>
@@ -420,15 +421,18 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
   }
   if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
   __syncthreads();
+  // each workgroup accumulates into its own slab row across launches (fixed
+  // order, deterministic); tfg_get_diag folds the rows when it is called
   double* bslab = slab + (int64_t)blockIdx.x * nb;
   for (int i = threadIdx.x; i < nb; i += kBlock) {
     double v = lds_bins[i];
     if ((i % 6) == 5) {
       for (int w = 1; w < kWaves; ++w) v = tfg::npmax(v, lds_bins[w * nb + i]);
+      bslab[i] = tfg::npmax(bslab[i], v);
     } else {
       for (int w = 1; w < kWaves; ++w) v += lds_bins[w * nb + i];
+      bslab[i] += v;
     }
-    bslab[i] = v;
   }
 }
 
@@ -446,7 +450,7 @@ __global__ void k_prepare_geo(const DevParams p, const R* __restrict__ stat, flo
   }
 }
 
-// acc[i] (+)= reduce over blocks of slab[b][i]; one workgroup per diag entry.
+// acc[i] = reduce over workgroups of slab[b][i]; one workgroup per diag entry.
 __global__ __launch_bounds__(kBlock) void k_diag_reduce(const double* __restrict__ slab, int nblocks, int nb,
                                                         double* __restrict__ acc) {
   __shared__ double red[kBlock];
@@ -466,7 +470,7 @@ __global__ __launch_bounds__(kBlock) void k_diag_reduce(const double* __restrict
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0) acc[i] = is_max ? tfg::npmax(acc[i], red[0]) : acc[i] + red[0];
+  if (threadIdx.x == 0) acc[i] = red[0];
 }
 
 template <class D, class S>
@@ -1155,7 +1159,7 @@ int tfg_init_state(tfg_handle* h) {
   HIPCHK(h, hipMemsetAsync(h->tot, 0, (size_t)h->n_pad * 8, h->stream));
   HIPCHK(h, hipMemsetAsync(h->ring, 0, (size_t)h->ring_len * h->n_pad * 4, h->stream));
   HIPCHK(h, hipMemsetAsync(h->hist, 0, (size_t)h->hist_depth * kNumHist * h->n_pad * h->rsz, h->stream));
-  HIPCHK(h, hipMemsetAsync(h->diag, 0, (size_t)h->n_catch * 6 * 8, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->slab, 0, (size_t)h->max_blocks * h->n_catch * 6 * 8, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->depths_derived = false;
   h->tot_dirty = false;
@@ -1206,7 +1210,6 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   const int64_t ngroups = h->n_pad / kCellsPerThread;
   const int blocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
-  const int nb = h->n_catch * 6;
   if (h->engine == TFG_F32 && h->geo_dirty) {
     hipLaunchKernelGGL((k_prepare_geo<float>), grid_for(h->n_pad), 256, 0, h->stream, h->dp, (const float*)h->stat,
                        h->geo, h->n_pad);
@@ -1220,8 +1223,6 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
                                     : launch_fused<double, true>(h, h->d_u + k0, K, blocks, lds);
     if (rc) return rc;
     h->depths_derived = true;
-    hipLaunchKernelGGL(k_diag_reduce, nb, kBlock, 0, h->stream, h->slab, blocks, nb, h->diag);
-    HIPCHK(h, hipGetLastError());
   }
   h->last_hist = u[nsteps - 1].hist;
   return TFG_OK;
@@ -1231,6 +1232,9 @@ int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
   if (!h || !out) return fail(h, TFG_ERR_ARG, "null argument");
   if (n_catch != h->n_catch) return fail(h, TFG_ERR_ARG, "n_catch mismatch");
   HIPCHK(h, hipSetDevice(h->device));
+  const int nb = n_catch * 6;
+  hipLaunchKernelGGL(k_diag_reduce, nb, kBlock, 0, h->stream, h->slab, h->max_blocks, nb, h->diag);
+  HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipMemcpyAsync(out, h->diag, (size_t)n_catch * 6 * 8, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   // P_max of an empty history is 0 like the reference's initial P_max (:314)
@@ -1241,7 +1245,7 @@ int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
 int tfg_reset_diag(tfg_handle* h) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipMemsetAsync(h->diag, 0, (size_t)h->n_catch * 6 * 8, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->slab, 0, (size_t)h->max_blocks * h->n_catch * 6 * 8, h->stream));
   return TFG_OK;
 }
 

@@ -156,6 +156,7 @@ class GlacierEngine:
 
     def uniforms(self, nsteps: int, frames=None) -> np.ndarray:
         k0 = self.step_index
+        default_frames = frames is None
         hist = (np.arange(k0, k0 + nsteps) % self.hist_depth).astype(np.int32)
         if frames is None:
             frames = (np.arange(k0, k0 + nsteps) % self.n_frames).astype(np.int32)
@@ -166,7 +167,10 @@ class GlacierEngine:
             if cache is None or cache[0] != b0:
                 cache = (b0, self.clock.uniforms(b0, self._UBLOCK))
                 self._ucache = cache
-            u = cache[1][k0 - b0:k0 - b0 + nsteps].copy()
+            u = cache[1][k0 - b0:k0 - b0 + nsteps]
+            if default_frames and self.n_frames == 1 and self.hist_depth == 1:
+                return u  # frame and slot 0: the cached records as they are (tfg_step copies them)
+            u = u.copy()
             u["frame"], u["hist"] = frames, hist
             return u
         return self.clock.uniforms(k0, nsteps, frames=frames, hist=hist)
