@@ -7,7 +7,7 @@ from pathlib import Path
 import numpy as np
 import yaml
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 from tests.harness import BASE_CFG, GOLDEN  # noqa: E402
 from topoflow_glacier import BmiTopoflowGlacier  # noqa: E402

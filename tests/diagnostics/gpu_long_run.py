@@ -2,14 +2,14 @@
 the fp32 engine on the synthetic workload for `steps` hourly steps; the
 outputs of every 24th step and the final state are saved to
 gpurun_out/long_run_<cells>x<steps>.npz for a CPU comparison with the oracle
-(scripts/long_run_compare.py).  Prints progress (flushed) as it goes."""
+(tests/diagnostics/long_run_compare.py).  Prints progress (flushed) as it goes."""
 import sys
 import time
 from pathlib import Path
 
 import numpy as np
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 from tests.harness import BASE_CFG, make_engine  # noqa: E402
 from topoflow_glacier.synthetic import diurnal_table  # noqa: E402

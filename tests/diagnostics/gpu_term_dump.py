@@ -5,7 +5,7 @@ from pathlib import Path
 
 import numpy as np
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 from tests.harness import BASE_CFG, make_engine  # noqa: E402
 from topoflow_glacier.synthetic import diurnal_table  # noqa: E402

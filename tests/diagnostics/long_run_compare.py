@@ -1,4 +1,4 @@
-"""Compare a GPU long run (scripts/gpu_long_run.py) with the oracle on CPU.
+"""Compare a GPU long run (tests/diagnostics/gpu_long_run.py) with the oracle on CPU.
 Prints, per variable, the floored relative error per month of
 model time and the fraction of cells above 1e-5.  Test infrastructure."""
 import sys
@@ -7,7 +7,7 @@ from pathlib import Path
 
 import numpy as np
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd"), str(ROOT / "oracle")]
 from tests.harness import oracle_synthetic, scale_floor  # noqa: E402
 
