@@ -553,7 +553,7 @@ __global__ void k_fill_synthetic(R* __restrict__ forc, R* __restrict__ stat, dou
   }
 }
 
-std::string g_err;  // errors before a handle exists
+thread_local std::string g_err;  // errors before a handle exists (per calling thread)
 
 inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
@@ -926,6 +926,8 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   if (!p || !out) return fail(nullptr, TFG_ERR_ARG, "null params/out");
   *out = nullptr;
   if (ny <= 0 || nx <= 0) return fail(nullptr, TFG_ERR_ARG, "grid must have ny, nx >= 1");
+  if (ny > (1ll << 31) || nx > (1ll << 31))  // before forming ny*nx
+    return fail(nullptr, TFG_ERR_ARG, "shard too large: ny and nx must stay below 2^31");
   if (engine != TFG_F32 && engine != TFG_F64) return fail(nullptr, TFG_ERR_ARG, "engine must be TFG_F32 or TFG_F64");
   if (n_frames < 1 || hist_depth < 1 || n_catch < 1) return fail(nullptr, TFG_ERR_ARG, "n_frames, hist_depth, n_catch must be >= 1");
   if (n_catch > 512) return fail(nullptr, TFG_ERR_ARG, "n_catch > 512 not supported");
