@@ -486,3 +486,46 @@ def test_batched_io_equals_per_field_io(engine):
             e.close()
     assert outs[0].shape == (8, n)
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("ny,nx", [(16, 16), (48, 100)])
+def test_bmi_grid_mode_vs_oracle(tmp_path, ny, nx):
+    """The drop-in BMI on a grid (ny/nx in the YAML, fp32 engine): per-cell
+    forcing arrays through set_value each step, outputs through get_value /
+    get_value_ptr, against the oracle on the same fp32-rounded inputs.  16x16
+    uses eager host mirrors, 48x100 the lazy ones."""
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    nsteps, seed = 12, 13
+    n = ny * nx
+    syn, _ = synthetic_inputs(seed, ny, nx, 24)
+    cfg = dict(BASE_CFG, ny=ny, nx=nx)
+    model = BmiTopoflowGlacier()
+    model.initialize(str(_write_cfg(tmp_path, cfg)))
+    assert model.get_var_nbytes("snowpack__depth") == 8 * n and model.get_grid_size(0) == n
+    names = {"P": "atmosphere_water__liquid_equivalent_precipitation_rate", "T_air": "land_surface_air__temperature",
+             "Hum_sp": "atmosphere_air_water~vapor__relative_saturation", "P_air": "land_surface_air__pressure",
+             "uz": "wind_speed_UV"}
+    for k in range(nsteps):
+        for v, bmi in names.items():
+            model.set_value(bmi, syn[v][k % 24].astype(np.float64))
+        model.update()
+    got = {v: model.get_value(b, np.zeros(n)).copy() for v, b in (("h_snow", "snowpack__depth"), ("SM", "snowpack__melt_volume_flux"),
+           ("IM", "glacier_ice__melt_volume_flux"), ("M_total", "land_surface_water__runoff_volume_flux"),
+           ("RH", "atmosphere_bottom_air_water-vapor__relative_saturation"), ("h_swe", "snowpack__liquid-equivalent_depth"),
+           ("h_iwe", "glacier__liquid_equivalent_depth"), ("h_ice", "glacier_ice__thickness"))}
+    ptr = model.get_value_ptr("snowpack__depth")
+    assert ptr.shape == (n,) and np.array_equal(ptr, got["h_snow"])
+    model.finalize()
+    r32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
+    forcing = {v: r32(syn[v][np.arange(nsteps) % 24]) for v in names}
+    static = {"elev": np.full(n, cfg["elev"]), "slope": np.full(n, cfg["slope"]), "aspect": np.full(n, cfg["aspect"]),
+              "h0_snow": np.full(n, cfg["h0_snow"]), "h0_ice": np.full(n, cfg["h0_ice"]),
+              "h0_swe": np.full(n, cfg["h0_swe"]), "h0_iwe": np.full(n, cfg["h0_iwe"])}
+    static = {k: r32(v) if k in ("elev", "slope", "aspect") else v for k, v in static.items()}
+    ref, _ = oracle_run(cfg, static, forcing, nsteps)
+    for v in ("h_snow", "SM", "IM", "M_total", "RH", "h_ice"):
+        err, _ = parity(got[v][None, :], ref[v][-1][None, :])
+        assert err <= 1e-5, (v, err)
+    for v in ("h_swe", "h_iwe"):
+        assert parity(got[v], ref[v][-1])[0] <= 1e-5, v
