@@ -89,3 +89,58 @@ def test_bulk_mode_equals_per_step_bmi(tmp_path):
         assert np.array_equal(a[k], b[k]), k
     assert a["h_swe"][-1] == b["h_swe"][-1] and a["h_iwe"][-1] == b["h_iwe"][-1]
     assert np.array_equal(a["routed"], b["routed"])
+
+
+@pytest.mark.gpu
+def test_integration_md_binding_stub_runs(tmp_path):
+    """The reference-side ctypes binding shown in INTEGRATION.md section 2,
+    executed as written (this package aliased as topoflow_glacier_mi355x, the
+    reference's _dynamic_input_vars / _output_vars in scope), drives a model
+    through the golden window and matches the drop-in BMI bit for bit."""
+    import re
+    import sys
+    import types
+
+    import topoflow_glacier
+    import topoflow_glacier._native
+    import topoflow_glacier.engine
+    import topoflow_glacier.physics.clock
+    from topoflow_glacier import BmiTopoflowGlacier
+    from topoflow_glacier.bmi import bmi_topoflow_glacier as btg
+    from topoflow_glacier.forcing import read_forcing_csv
+    from tests.harness import ROOT
+
+    text = (ROOT / "INTEGRATION.md").read_text()
+    code = re.search(r"```python\n(# in the reference's bmi_topoflow_glacier.py\n.*?)```", text, re.S).group(1)
+    alias = {"topoflow_glacier_mi355x": topoflow_glacier, "topoflow_glacier_mi355x._native": topoflow_glacier._native,
+             "topoflow_glacier_mi355x.engine": topoflow_glacier.engine,
+             "topoflow_glacier_mi355x.physics.clock": topoflow_glacier.physics.clock}
+    saved = {k: sys.modules.get(k) for k in alias}
+    sys.modules.update(alias)
+    try:
+        ns = {"_dynamic_input_vars": btg._dynamic_input_vars, "_output_vars": btg._output_vars}
+        exec(compile(code, "INTEGRATION.md", "exec"), ns)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                sys.modules.pop(k, None)
+            else:
+                sys.modules[k] = v
+    cfg = tmp_path / "cat.yaml"
+    cfg.write_text(yaml.dump(BASE_CFG))
+    t = read_forcing_csv(CSV, BASE_CFG["start_time"], BASE_CFG["end_time"])
+    host = BmiTopoflowGlacier()  # supplies cfg + the (1,) arrays, like the reference model object
+    host.initialize(cfg)
+    stub = ns["_GpuUpdate"](host)
+    ref = BmiTopoflowGlacier()
+    ref.initialize(cfg)
+    for i in range(48):
+        t.apply(host, i)
+        stub.update()
+        t.apply(ref, i)
+        ref.update()
+        for name in ns["OUT_ID"]:
+            assert host.get_value_ptr(name)[0] == ref.get_value(name, np.zeros(1))[0], (i, name)
+    stub.close()
+    host.finalize()
+    ref.finalize()
