@@ -179,8 +179,11 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_MIN_WAVES
 #define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
 #endif
+#ifndef TFG_MIN_WAVES_EXACT
+#define TFG_MIN_WAVES_EXACT 2  // fp64 engine: 256 VGPRs, no scratch spills
+#endif
 template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
-__global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+__global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
                                                   const float* __restrict__ geo,   // [kGeoF][n_pad] f32 + [2][n_pad] f64
@@ -361,6 +364,15 @@ __global__ __launch_bounds__(kBlock, TFG_MIN_WAVES) void k_fused(const KArgs a, 
 #else
       Frame fa, fb;
       fetch(0, fa);
+      if constexpr (EXACT) {
+        // the fp64 step is issue-bound and register-heavy: one copy of its
+        // body (not two interleaved) keeps it within 256 VGPRs
+        for (int k = 0; k < a.K; ++k) {
+          fetch(k + 1, fb);
+          advance(k, fa);
+          fa = fb;
+        }
+      } else
       for (int k = 0; k < a.K; k += 2) {
         fetch(k + 1, fb);
         advance(k, fa);
