@@ -189,6 +189,16 @@ int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int
  * Replaces: the per-step get_value() calls (:1810-1822). */
 int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n, int dst_on_device);
 
+/* One synchronous model step for callers that step from the host (the BMI's
+ * update(), :413-465): the same as tfg_set_inputs(h, frame, src, ...) +
+ * tfg_step(h, u, 1) + tfg_get_outputs(h, u->hist, dst, ...), with u->frame ==
+ * frame, but the kernels read src and u and write dst through one pinned,
+ * device-mapped block (no staging copies) and the call returns with dst
+ * filled.  src[5][n] / dst[8][n] are host buffers in the orders of
+ * tfg_set_inputs / tfg_get_outputs. */
+int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
+               int dst_dtype, int64_t n);
+
 /* Copy n cells of a field out.  `index` is the history slot for TFG_OUT_*
  * (except H_SWE/H_IWE, which are state), the frame for TFG_IN_*.
  * Replaces: get_value / get_value_ptr (:1810-1828). */

@@ -58,6 +58,7 @@ E.GlacierEngine.set_inputs = timed("set_inputs", E.GlacierEngine.set_inputs)
 E.GlacierEngine.run = timed("run (uniforms + tfg_step)", E.GlacierEngine.run)
 E.GlacierEngine.uniforms = timed("  uniforms (Python)", E.GlacierEngine.uniforms)
 E.GlacierEngine.get_outputs = timed("get_outputs", E.GlacierEngine.get_outputs)
+E.GlacierEngine.update_io = timed("update_io (tfg_update)", E.GlacierEngine.update_io)
 m = BmiTopoflowGlacier()
 m.initialize(cfg)
 t0 = time.perf_counter()

@@ -488,6 +488,45 @@ def test_batched_io_equals_per_field_io(engine):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+@pytest.mark.parametrize("engine", ["float32", "float64"])
+@pytest.mark.parametrize("frames,hist", [(1, 1), (3, 2)])
+def test_update_io_equals_set_step_get(engine, frames, hist):
+    """tfg_update (one synchronous call through the pinned, device-mapped
+    block) == tfg_set_inputs + tfg_step + tfg_get_outputs, bit for bit, on a
+    padded grid; (1, 1) is the BMI's cached-uniforms path."""
+    ny, nx, n = 5, 13, 65
+    syn, d = synthetic_inputs(22, ny, nx, 24)
+    names = ("P_air", "Hum_sp", "P", "T_air", "uz")
+    outs = []
+    for fused_call in (False, True):
+        e = make_engine(BASE_CFG, ny, nx, engine, n_frames=frames, hist_depth=hist)
+        seq = []
+        try:
+            e.fill_synthetic(22, np.resize(d, frames))
+            buf = np.empty((8, n))
+            for k in range(7):
+                vals = np.ascontiguousarray(np.stack([syn[v][k].astype(np.float64) for v in names]))
+                if fused_call:
+                    seq.append(e.update_io(vals, buf).copy())
+                else:
+                    e.set_inputs(vals, k % frames)
+                    e.run(1)
+                    seq.append(e.get_outputs())
+            seq.append(e.get_field("Eccs"))
+            seq.append(e.diagnostics())
+        finally:
+            e.close()
+        outs.append(seq)
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    e = make_engine(BASE_CFG, ny, nx, engine, n_frames=1, hist_depth=1)
+    try:
+        with pytest.raises(ValueError):
+            e.update_io(np.zeros((5, n), dtype=np.float32), np.zeros((8, n)))
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("ny,nx", [(16, 16), (48, 100)])
 def test_bmi_grid_mode_vs_oracle(tmp_path, ny, nx):
     """The drop-in BMI on a grid (ny/nx in the YAML, fp32 engine): per-cell

@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <new>
 #include <string>
@@ -68,6 +70,14 @@ struct KArgs {
   int K;
   int n_catch;
   int64_t n, n_pad;
+  // tfg_update (K == 1): the step's forcing [kNumForc][n_pad] (engine type)
+  // is read from io_in, a device-mapped pinned host block, and also written to
+  // its frame; the eight BMI outputs go to io_out [8][n] fp64 in the same block.
+  // Null for every other launch.
+  const void* io_in;
+  double* io_out;
+  uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
+  uint32_t io_seq;
 };
 
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
@@ -227,17 +237,17 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       const int64_t c0 = g * C;
       const uint32_t lc = (uint32_t)c0;  // element index within every field
       if constexpr (CATCH) iload<C>(catch_id, lc, cid);
-      // static rasters: exact engine derives the geometry in fp64 here; the
-      // fast engine reads the planes k_prepare_geo wrote
+      // static geometry: the planes k_prepare_static (exact engine, fp64 in
+      // reference op order) or k_prepare_geo (fast engine) wrote
       CellStatic SX[EXACT ? C : 1];
       tfg::CellStaticF SF[EXACT ? 1 : C];
       if constexpr (EXACT) {
-        R el[C], sl[C], as[C];
-        vload<R, C>(stat, lc, el);
-        vload<R, C>(stat + n_pad, lc, sl);
-        vload<R, C>(stat + 2 * n_pad, lc, as);
+        const double* gx = reinterpret_cast<const double*>(geo);
+        double v[6][C];
 #pragma unroll
-        for (int j = 0; j < C; ++j) SX[j] = tfg::derive_static(p, (double)el[j], (double)sl[j], (double)as[j]);
+        for (int f = 0; f < 6; ++f) dload<C>(gx + f * n_pad, lc, v[f]);
+#pragma unroll
+        for (int j = 0; j < C; ++j) SX[j] = {v[0][j], v[1][j], v[2][j], v[3][j], v[4][j], v[5][j]};
       } else {
         float gv[tfg::kGeoF][C];
 #pragma unroll
@@ -305,7 +315,8 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       struct Frame { R P[C], T[C], Q[C], PA[C], UZ[C]; int32_t q[C]; };
       auto fetch = [&](int k, Frame& f) {
         const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
-        const R* __restrict__ fr = forc + (int64_t)un->frame * kNumForc * n_pad;
+        const R* __restrict__ fr =
+            a.io_in ? static_cast<const R*>(a.io_in) : forc + (int64_t)un->frame * kNumForc * n_pad;
         static_assert(C == 1, "streamed step accesses are per cell");
         static_assert(sizeof(R) == 4 || sizeof(R) == 8, "R is float or double");
         const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
@@ -380,6 +391,29 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
         if (k + 1 < a.K) advance(k + 1, fb);
       }
 #endif
+      if (a.io_in) {  // tfg_update: the frame keeps the inputs, outputs go to the host block
+        const int fidx = uni[0].frame, hidx = uni[0].hist;
+        R* __restrict__ fr = const_cast<R*>(forc) + (int64_t)fidx * kNumForc * n_pad;
+        const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
+        sstore(fr + F_P * n_pad, oR, fa.P[0]);
+        sstore(fr + F_T * n_pad, oR, fa.T[0]);
+        sstore(fr + F_Q * n_pad, oR, fa.Q[0]);
+        sstore(fr + F_PA * n_pad, oR, fa.PA[0]);
+        sstore(fr + F_UZ * n_pad, oR, fa.UZ[0]);
+        if (c0 < a.n) {
+          const R* hs = hist + (int64_t)hidx * kNumHist * n_pad + c0;
+          double* o = a.io_out + c0;
+          const int64_t n = a.n;
+          o[0 * n] = (double)hs[H_HSNOW * n_pad];
+          o[1 * n] = cs[0].h_swe;
+          o[2 * n] = (double)hs[H_SM * n_pad];
+          o[3 * n] = (double)hs[H_HICE * n_pad];
+          o[4 * n] = cs[0].h_iwe;
+          o[5 * n] = (double)hs[H_IM * n_pad];
+          o[6 * n] = (double)hs[H_MTOT * n_pad];
+          o[7 * n] = (double)hs[H_RH * n_pad];
+        }
+      }
       // fast engine: fold the cell's partial sums into the fp64 accumulators
       // with the constant factors of :567, :585-623, :1486, :1493 (padding
       // cells excluded)
@@ -446,6 +480,12 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       bslab[i] += v;
     }
   }
+  if (a.io_flag) {  // tfg_update: tell the waiting host this workgroup is done
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(a.io_flag + blockIdx.x, a.io_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Per-cell solar geometry of the fast engine, once per static-raster change:
@@ -459,6 +499,22 @@ __global__ void k_prepare_geo(const DevParams p, const R* __restrict__ stat, flo
     for (int f = 0; f < tfg::kGeoF; ++f) geo[f * n_pad + i] = g.f[f];
     gd[i] = g.tan_eq;
     gd[n_pad + i] = g.t_noon;
+  }
+}
+
+// Exact engine: CellStatic planes [6][n_pad] fp64 (elev, cos_leq, sin_leq,
+// dlon, tan_eq, t_noon), derived once per static-raster change instead of
+// once per launch.
+template <class R>
+__global__ void k_prepare_static(const DevParams p, const R* __restrict__ stat, double* __restrict__ gx, int64_t n_pad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
+    const CellStatic s = tfg::derive_static(p, (double)stat[i], (double)stat[n_pad + i], (double)stat[2 * n_pad + i]);
+    gx[i] = s.elev;
+    gx[n_pad + i] = s.cos_leq;
+    gx[2 * n_pad + i] = s.sin_leq;
+    gx[3 * n_pad + i] = s.dlon;
+    gx[4 * n_pad + i] = s.tan_eq;
+    gx[5 * n_pad + i] = s.t_noon;
   }
 }
 
@@ -655,7 +711,7 @@ struct tfg_handle {
   void* forc = nullptr;
   void* stat = nullptr;
   void* lwsw = nullptr;          // [2][n_pad] R, not read by the physics
-  float* geo = nullptr;          // fast engine: [5][n_pad] f32 + [2][n_pad] f64 solar geometry
+  float* geo = nullptr;          // fast engine: [5][n_pad] f32 + [2][n_pad] f64 solar geometry; exact: [6][n_pad] f64 CellStatic
   bool geo_dirty = true;
   int32_t* catch_id = nullptr;
   double* st = nullptr;
@@ -692,6 +748,12 @@ struct tfg_handle {
   void* out_d = nullptr;
   void* out_h = nullptr;
   size_t out_cap = 0;
+  // tfg_update: one pinned host block (inputs | uniforms | outputs) that the
+  // kernels read and write directly through its device mapping
+  char* io_h = nullptr;
+  char* io_d = nullptr;
+  size_t io_cap = 0;
+  uint32_t io_seq = 0;
   int64_t last_hist = 0;
   std::string err;
 };
@@ -892,11 +954,23 @@ void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {
 bool is_frame_field(int f) { return f == TFG_IN_P || f == TFG_IN_T_AIR || f == TFG_IN_HUM_SP || f == TFG_IN_P_AIR || f == TFG_IN_UZ; }
 bool is_hist_field(int f) { return f == TFG_OUT_H_SNOW || f == TFG_OUT_SM || f == TFG_OUT_H_ICE || f == TFG_OUT_IM || f == TFG_OUT_M_TOTAL || f == TFG_OUT_RH; }
 
+// tfg_update's single-step launch (KArgs::io_*); empty for every other launch
+struct IoArgs {
+  const void* in = nullptr;
+  double* out = nullptr;
+  uint32_t* flag = nullptr;
+  uint32_t seq = 0;
+};
+
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds) {
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io = IoArgs()) {
   KArgs a;
   a.p = h->dp;
   a.K = K;
+  a.io_in = io.in;
+  a.io_out = io.out;
+  a.io_flag = io.flag;
+  a.io_seq = io.seq;
   a.n_catch = h->n_catch;
   a.n = h->n;
   a.n_pad = h->n_pad;
@@ -993,7 +1067,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {&h->forc, (size_t)n_frames * kNumForc * np * rs},
       {&h->stat, 3 * (size_t)np * rs},
       {&h->lwsw, 2 * (size_t)np * rs},
-      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (tfg::kGeoF * 4 + 2 * 8) : 16},
+      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (tfg::kGeoF * 4 + 2 * 8) : (size_t)np * 6 * 8},
       {(void**)&h->st, (size_t)kNumState * np * 8},
       {(void**)&h->tot, (size_t)np * 8},
       {(void**)&h->ring, (size_t)p->ring_len * np * 4},
@@ -1031,6 +1105,7 @@ int tfg_destroy(tfg_handle* h) {
   }
   if (h->out_d) (void)hipFree(h->out_d);
   if (h->out_h) (void)hipHostFree(h->out_h);
+  if (h->io_h) (void)hipHostFree(h->io_h);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return TFG_OK;
@@ -1181,9 +1256,9 @@ int tfg_init_state(tfg_handle* h) {
   return TFG_OK;
 }
 
-int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
-  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
-  if (nsteps <= 0) return TFG_OK;
+namespace {
+
+int check_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   if (!u) return fail(h, TFG_ERR_ARG, "null uniforms");
   if (!h->initialised) return fail(h, TFG_ERR_STATE, "tfg_init_state() has not been called");
   if (h->slope_invalid) return fail(h, TFG_ERR_DOMAIN, "slope raster invalid (bmi_topoflow_glacier.py:1106-1111)");
@@ -1192,12 +1267,54 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
     if (u[k].hist < 0 || u[k].hist >= h->hist_depth) return fail(h, TFG_ERR_ARG, "uniforms: hist slot out of range");
     if (u[k].slot < 0 || u[k].slot >= h->ring_len) return fail(h, TFG_ERR_ARG, "uniforms: ring slot out of range");
   }
-  HIPCHK(h, hipSetDevice(h->device));
+  return TFG_OK;
+}
+
+// The launches of nsteps steps whose uniforms the device reads at d_u (u is
+// the host copy of the same records).
+int fused_blocks(const tfg_handle* h) {
+  const int64_t ngroups = h->n_pad / kCellsPerThread;
+  return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
+}
+
+int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
+                 const IoArgs& io = IoArgs()) {
   if (h->tot_dirty) {  // window slots were set: rebuild the running totals
     hipLaunchKernelGGL(k_window_total, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->ring, h->ring_len, h->n_pad);
     HIPCHK(h, hipGetLastError());
     h->tot_dirty = false;
   }
+  const int blocks = fused_blocks(h);
+  const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
+  if (h->geo_dirty) {
+    if (h->engine == TFG_F32)
+      hipLaunchKernelGGL((k_prepare_geo<float>), grid_for(h->n_pad), 256, 0, h->stream, h->dp, (const float*)h->stat,
+                         h->geo, h->n_pad);
+    else
+      hipLaunchKernelGGL((k_prepare_static<double>), grid_for(h->n_pad), 256, 0, h->stream, h->dp,
+                         (const double*)h->stat, reinterpret_cast<double*>(h->geo), h->n_pad);
+    HIPCHK(h, hipGetLastError());
+    h->geo_dirty = false;
+  }
+  const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
+  for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
+    const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
+    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io)
+                                    : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io);
+    if (rc) return rc;
+    h->depths_derived = true;
+  }
+  h->last_hist = u[nsteps - 1].hist;
+  return TFG_OK;
+}
+
+}  // namespace
+
+int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (nsteps <= 0) return TFG_OK;
+  if (int rc = check_step(h, u, nsteps)) return rc;
+  HIPCHK(h, hipSetDevice(h->device));
   // stage uniforms: pinned double buffer -> device array
   const int b = h->h_u_next;
   h->h_u_next ^= 1;
@@ -1220,26 +1337,7 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   std::memcpy(h->h_u[b], u, (size_t)nsteps * sizeof(tfg_uniforms));
   HIPCHK(h, hipMemcpyAsync(h->d_u, h->h_u[b], (size_t)nsteps * sizeof(tfg_uniforms), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipEventRecord(h->h_u_ev[b], h->stream));
-
-  const int64_t ngroups = h->n_pad / kCellsPerThread;
-  const int blocks = (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
-  const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
-  if (h->engine == TFG_F32 && h->geo_dirty) {
-    hipLaunchKernelGGL((k_prepare_geo<float>), grid_for(h->n_pad), 256, 0, h->stream, h->dp, (const float*)h->stat,
-                       h->geo, h->n_pad);
-    HIPCHK(h, hipGetLastError());
-    h->geo_dirty = false;
-  }
-  const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
-  for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
-    const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
-    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, h->d_u + k0, K, blocks, lds)
-                                    : launch_fused<double, true>(h, h->d_u + k0, K, blocks, lds);
-    if (rc) return rc;
-    h->depths_derived = true;
-  }
-  h->last_hist = u[nsteps - 1].hist;
-  return TFG_OK;
+  return launch_steps(h, h->d_u, u, nsteps);
 }
 
 int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
@@ -1292,6 +1390,11 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
   return tfg_init_state(h);
 }
 
+namespace {
+int launch_scatter(tfg_handle* h, int frame, const void* dsrc, int src_dtype, int64_t n);
+int launch_gather(tfg_handle* h, int hist, void* gdst, int dst_dtype, int64_t n);
+}  // namespace
+
 int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int64_t n, int src_on_device) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!src) return fail(h, TFG_ERR_ARG, "null src");
@@ -1322,6 +1425,15 @@ int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int
     HIPCHK(h, hipMemcpyAsync(h->in_d[b], h->in_h[b], bytes, hipMemcpyHostToDevice, h->stream));
     dsrc = h->in_d[b];
   }
+  if (int rc = launch_scatter(h, frame, dsrc, src_dtype, n)) return rc;
+  if (b >= 0) HIPCHK(h, hipEventRecord(h->in_ev[b], h->stream));
+  return TFG_OK;
+}
+
+namespace {
+
+// frame <- src[5][n] (device-visible pointer)
+int launch_scatter(tfg_handle* h, int frame, const void* dsrc, int src_dtype, int64_t n) {
   char* fr = static_cast<char*>(h->forc) + (size_t)frame * kNumForc * h->n_pad * h->rsz;
   const int gb = grid_for(n);
   if (h->engine == TFG_F32 && src_dtype == TFG_F32)
@@ -1333,9 +1445,27 @@ int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int
   else
     hipLaunchKernelGGL((k_scatter_inputs<double, double>), gb, 256, 0, h->stream, (double*)fr, (const double*)dsrc, n, h->n_pad);
   HIPCHK(h, hipGetLastError());
-  if (b >= 0) HIPCHK(h, hipEventRecord(h->in_ev[b], h->stream));
   return TFG_OK;
 }
+
+// dst[8][n] (device-visible pointer) <- outputs of history slot `hist`
+int launch_gather(tfg_handle* h, int hist, void* gdst, int dst_dtype, int64_t n) {
+  const char* hs = static_cast<const char*>(h->hist) + (size_t)hist * kNumHist * h->n_pad * h->rsz;
+  const int from_state = h->depths_derived ? 0 : 1;
+  const int gb = grid_for(n);
+  if (h->engine == TFG_F32 && dst_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<float, float>), gb, 256, 0, h->stream, (float*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
+  else if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<float, double>), gb, 256, 0, h->stream, (double*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
+  else if (dst_dtype == TFG_F32)
+    hipLaunchKernelGGL((k_gather_outputs<double, float>), gb, 256, 0, h->stream, (float*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
+  else
+    hipLaunchKernelGGL((k_gather_outputs<double, double>), gb, 256, 0, h->stream, (double*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
+  HIPCHK(h, hipGetLastError());
+  return TFG_OK;
+}
+
+}  // namespace
 
 int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
@@ -1358,23 +1488,86 @@ int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n
     }
     gdst = h->out_d;
   }
-  const char* hs = static_cast<const char*>(h->hist) + (size_t)hist * kNumHist * h->n_pad * h->rsz;
-  const int from_state = h->depths_derived ? 0 : 1;
-  const int gb = grid_for(n);
-  if (h->engine == TFG_F32 && dst_dtype == TFG_F32)
-    hipLaunchKernelGGL((k_gather_outputs<float, float>), gb, 256, 0, h->stream, (float*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
-  else if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_gather_outputs<float, double>), gb, 256, 0, h->stream, (double*)gdst, (const float*)hs, h->st, n, h->n_pad, from_state);
-  else if (dst_dtype == TFG_F32)
-    hipLaunchKernelGGL((k_gather_outputs<double, float>), gb, 256, 0, h->stream, (float*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
-  else
-    hipLaunchKernelGGL((k_gather_outputs<double, double>), gb, 256, 0, h->stream, (double*)gdst, (const double*)hs, h->st, n, h->n_pad, from_state);
-  HIPCHK(h, hipGetLastError());
+  if (int rc = launch_gather(h, hist, gdst, dst_dtype, n)) return rc;
   if (!dst_on_device) {
     HIPCHK(h, hipMemcpyAsync(h->out_h, h->out_d, bytes, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     std::memcpy(dst, h->out_h, bytes);
   }
+  return TFG_OK;
+}
+
+int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
+               int dst_dtype, int64_t n) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!src || !dst) return fail(h, TFG_ERR_ARG, "null src/dst");
+  if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
+  if (frame < 0 || frame >= h->n_frames) return fail(h, TFG_ERR_ARG, "frame index out of range");
+  if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+  if (int rc = check_step(h, u, 1)) return rc;
+  if (u->frame != frame) return fail(h, TFG_ERR_ARG, "uniforms: frame differs from the input frame");
+  HIPCHK(h, hipSetDevice(h->device));
+  // One pinned block [forcing kNumForc x n_pad (engine type) | uniforms | outputs 8 x n f64];
+  // the call is synchronous, so one block suffices.
+  const int64_t np = h->n_pad;
+  const size_t in_b = (size_t)kNumForc * np * h->rsz;
+  const size_t u_off = (in_b + 255) & ~(size_t)255;
+  const size_t out_off = u_off + 256;
+  const size_t out_b = (size_t)8 * n * 8;
+  const int blocks = fused_blocks(h);
+  const size_t flag_off = (out_off + out_b + 255) & ~(size_t)255;
+  const size_t total = flag_off + (size_t)blocks * 4;
+  if (h->io_cap < total) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->io_h) HIPCHK(h, hipHostFree(h->io_h));
+    h->io_h = h->io_d = nullptr;
+    h->io_cap = 0;
+    HIPCHK(h, hipHostMalloc((void**)&h->io_h, total, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h->io_h, 0, total);  // padding cells read zeros; flags start at 0
+    HIPCHK(h, hipHostGetDevicePointer((void**)&h->io_d, h->io_h, 0));
+    h->io_cap = total;
+    h->io_seq = 0;
+  }
+  // BMI order (P_air, Hum_sp, P, T_air, uz) -> frame fields, converted to the engine type
+  static const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};
+  for (int f = 0; f < 5; ++f) {
+    char* o = h->io_h + (size_t)map[f] * np * h->rsz;
+    if (src_dtype == TFG_F64) {
+      const double* sv = static_cast<const double*>(src) + (size_t)f * n;
+      if (h->engine == TFG_F32) for (int64_t i = 0; i < n; ++i) reinterpret_cast<float*>(o)[i] = (float)sv[i];
+      else std::memcpy(o, sv, (size_t)n * 8);
+    } else {
+      const float* sv = static_cast<const float*>(src) + (size_t)f * n;
+      if (h->engine == TFG_F32) std::memcpy(o, sv, (size_t)n * 4);
+      else for (int64_t i = 0; i < n; ++i) reinterpret_cast<double*>(o)[i] = (double)sv[i];
+    }
+  }
+  std::memcpy(h->io_h + u_off, u, sizeof(tfg_uniforms));
+  IoArgs io;
+  io.in = h->io_d;
+  io.out = reinterpret_cast<double*>(h->io_d + out_off);
+  io.flag = reinterpret_cast<uint32_t*>(h->io_d + flag_off);
+  io.seq = ++h->io_seq == 0 ? ++h->io_seq : h->io_seq;  // never 0, the initial flag value
+  if (int rc = launch_steps(h, reinterpret_cast<const tfg_uniforms*>(h->io_d + u_off), u, 1, io)) return rc;
+  // Wait for the workgroups' release flags (a few microseconds sooner than a
+  // stream synchronisation); after ~2 ms fall back to the stream wait, which
+  // also reports a failed launch.
+  {
+    const volatile uint32_t* fl = reinterpret_cast<const volatile uint32_t*>(h->io_h + flag_off);
+    const auto t0 = std::chrono::steady_clock::now();
+    bool done = false;
+    for (int64_t spins = 0; !done; ++spins) {
+      done = true;
+      for (int b = 0; b < blocks && done; ++b) done = fl[b] == io.seq;
+      if (!done && (spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+    }
+    if (done) std::atomic_thread_fence(std::memory_order_acquire);
+    else HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  const double* oh = reinterpret_cast<const double*>(h->io_h + out_off);
+  if (dst_dtype == TFG_F64) std::memcpy(dst, oh, out_b);
+  else for (int64_t i = 0; i < 8 * n; ++i) static_cast<float*>(dst)[i] = (float)oh[i];
   return TFG_OK;
 }
 

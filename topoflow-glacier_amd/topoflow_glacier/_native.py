@@ -98,6 +98,7 @@ def load() -> ctypes.CDLL:
         "tfg_terrain_from_dem": ([vp, ctypes.c_double, ctypes.c_double, vp, vp, i32, i32], i32),
         "tfg_set_inputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
+        "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -127,4 +128,5 @@ def exported_symbols() -> list[str]:
         "tfg_set_stream", "tfg_get_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_set_inputs", "tfg_get_outputs",
+        "tfg_update",
     ) if hasattr(L, n)]

@@ -204,6 +204,9 @@ class BmiTopoflowGlacier(BmiBase):
         self._eager = n <= _EAGER_MAX_CELLS
         self._in_block = np.empty((5, n), dtype=np.float64)
         self._out_block = np.empty((8, n), dtype=np.float64)
+        # the mirrors are updated in place (Context.set_value), so resolve them once
+        self._in_mirrors = [self._dynamic_inputs.value(_ext(name)) for name in _INPUT_BLOCK]
+        self._out_mirrors = [self._outputs.value(name) for name, _ in _output_vars]
         self._engine = make_engine(cfg)
         self._beta_invalid = configure_engine(self._engine, cfg)
         for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
@@ -216,11 +219,8 @@ class BmiTopoflowGlacier(BmiBase):
         end = parse_time(cfg.end_time)
         self.end_year, self.end_month, self.end_day, self.end_hour = end.year, end.month, end.day, end.hour
         self.start_time = start
-        self.start_datetime = start  # advanced each step, as in the reference (:1866-1893)
-        self.year = start.year
-        self.julian_day = None
-        self.TSN_offset = None
-        self.GMT_offset = None
+        self._cal = (0, start, start.year, None, None, None)
+        self._clock = self._engine.clock
 
     # ----------------------------------------------------------------- update
     def _require(self) -> GlacierEngine:
@@ -237,26 +237,55 @@ class BmiTopoflowGlacier(BmiBase):
         for i, name in enumerate(_INPUT_BLOCK):  # one transfer for the five inputs (tfg_set_inputs)
             block[i] = np.broadcast_to(self._dynamic_inputs.value(_ext(name)), (n,))
         eng.set_inputs(block, 0)
+        self._push_dirty_outputs()
+
+    def _push_dirty_outputs(self) -> None:
         for name in sorted(self._dirty_outputs):
-            eng.set_field(name, self._outputs.value(_ext(name)))
+            self._engine.set_field(name, self._outputs.value(_ext(name)))
         self._dirty_outputs.clear()
 
     def _after_steps(self, nsteps: int) -> None:
-        k = self._timestep + nsteps - 1
-        jd, yr, gmt, tsn = self._engine.clock.calendar(k, 1)
-        self.julian_day, self.year, self.GMT_offset, self.TSN_offset = float(jd[0]), int(yr[0]), float(gmt[0]), float(tsn[0])
-        self.start_datetime = self.start_time + timedelta(hours=self.dt * (k + 1))
         self._timestep += nsteps
         self._stale = {_int(n) for n, _ in _output_vars}
         if self._eager:
             self._refresh_all()
 
+    # The reference's per-step clock attributes (update_julian_day :957-1004,
+    # get_current_datetime :1866-1893), computed when read rather than every step.
+    def _calendar(self) -> tuple:
+        if self._cal[0] != self._timestep:
+            k = self._timestep - 1
+            jd, yr, gmt, tsn = self._clock.calendar(k, 1)
+            self._cal = (self._timestep, self.start_time + timedelta(hours=self.dt * (k + 1)), int(yr[0]),
+                         float(jd[0]), float(gmt[0]), float(tsn[0]))
+        return self._cal
+
+    start_datetime = property(lambda self: self._calendar()[1])
+    year = property(lambda self: self._calendar()[2])
+    julian_day = property(lambda self: self._calendar()[3])
+    GMT_offset = property(lambda self: self._calendar()[4])
+    TSN_offset = property(lambda self: self._calendar()[5])
+
     def update(self) -> None:
-        """Advance one time step (reference :413-465) on the GPU."""
+        """Advance one time step (reference :413-465) on the GPU.  Small
+        models (eager mirrors) take one synchronous tfg_update call: inputs in,
+        one step, all eight outputs back."""
         eng = self._require()
-        self._push_inputs()
-        eng.run(1)
-        self._after_steps(1)
+        if not self._eager:
+            self._push_inputs()
+            eng.run(1)
+            self._after_steps(1)
+            return
+        if self._dirty_outputs:
+            self._push_dirty_outputs()
+        block = self._in_block
+        for i, v in enumerate(self._in_mirrors):
+            block[i] = v
+        out = eng.update_io(block, self._out_block)
+        self._timestep += 1
+        for dst, row in zip(self._out_mirrors, out):
+            dst[:] = row
+        self._stale.clear()
 
     def update_until(self, time: float) -> None:
         """Advance to `time` [s] with one fused multi-step run (reference :471-490)."""

@@ -187,6 +187,32 @@ class GlacierEngine:
         self._chk(self.lib.tfg_step(self.h, u.ctypes.data_as(ctypes.c_void_p), nsteps))
         self.step_index += nsteps
 
+    def update_io(self, values: np.ndarray, out: np.ndarray) -> np.ndarray:
+        """One synchronous step fed from the host (tfg_update): inputs
+        values[5][n] (P_air, Hum_sp, P, T_air, uz), outputs out[8][n] (h_snow,
+        h_swe, SM, h_ice, h_iwe, IM, M_total, RH); both C-contiguous float64.
+        This is BMI update()'s per-step path (:413-465)."""
+        if values.shape != (5, self.n) or out.shape != (8, self.n) or values.dtype != np.float64 \
+                or out.dtype != np.float64 or not (values.flags.c_contiguous and out.flags.c_contiguous):
+            raise ValueError(f"update_io needs C-contiguous float64 [5][{self.n}] and [8][{self.n}]")
+        k0 = self.step_index
+        frame = k0 % self.n_frames
+        if self.n_frames == 1 and self.hist_depth == 1:
+            # the cached block's records have frame = hist = 0: pass one by address
+            b0 = k0 - k0 % self._UBLOCK
+            cache = getattr(self, "_ucache", None)
+            if cache is None or cache[0] != b0:
+                cache = (b0, self.clock.uniforms(b0, self._UBLOCK))
+                self._ucache = cache
+            uptr = cache[1].ctypes.data + (k0 - b0) * nat.UNIFORM_DTYPE.itemsize
+            keep = None
+        else:
+            keep = np.ascontiguousarray(self.uniforms(1), dtype=nat.UNIFORM_DTYPE)
+            uptr = keep.ctypes.data
+        self._chk(self.lib.tfg_update(self.h, frame, values.ctypes.data, nat.F64, uptr, out.ctypes.data, nat.F64, self.n))
+        self.step_index += 1
+        return out
+
     def sync(self) -> None:
         self._chk(self.lib.tfg_sync(self.h))
 
