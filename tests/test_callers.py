@@ -144,3 +144,49 @@ def test_integration_md_binding_stub_runs(tmp_path):
     stub.close()
     host.finalize()
     ref.finalize()
+
+
+@pytest.mark.gpu
+def test_many_bmi_instances_in_one_process_interleaved(tmp_path):
+    """NextGen holds one model instance per catchment in one process and steps
+    them in turn.  Twelve instances (the reference's catchment configs, two
+    each) stepped round-robin through the golden forcing equal each config's
+    solo run bit for bit: handles share nothing."""
+    from pathlib import Path
+
+    from topoflow_glacier import BmiTopoflowGlacier
+    from topoflow_glacier.forcing import read_forcing_csv
+    from tests.harness import ROOT
+
+    cfgs = sorted((ROOT / "tests" / "golden" / "config").glob("cat-*.yaml"))
+    assert len(cfgs) == 6
+    t = read_forcing_csv(CSV, BASE_CFG["start_time"], BASE_CFG["end_time"])
+    nsteps = 36
+    names = ["snowpack__depth", "glacier_ice__thickness", "land_surface_water__runoff_volume_flux",
+             "snowpack__melt_volume_flux", "glacier_ice__melt_volume_flux"]
+
+    def run(models):
+        rec = [[] for _ in models]
+        for i in range(nsteps):
+            for j, m in enumerate(models):
+                t.apply(m, i)
+                m.update()
+                rec[j].append([m.get_value(v, np.zeros(1))[0] for v in names])
+        return [np.array(r) for r in rec]
+
+    def make(p: Path):
+        m = BmiTopoflowGlacier()
+        m.initialize(p)
+        return m
+
+    models = [make(p) for p in cfgs for _ in range(2)]
+    inter = run(models)
+    for m in models:
+        m.finalize()
+    for j, p in enumerate(cfgs):
+        solo = make(p)
+        ref = run([solo])[0]
+        solo.finalize()
+        np.testing.assert_array_equal(inter[2 * j], ref, err_msg=p.name)
+        np.testing.assert_array_equal(inter[2 * j + 1], ref, err_msg=p.name)
+    assert not np.array_equal(inter[0], inter[-1])  # the configs differ

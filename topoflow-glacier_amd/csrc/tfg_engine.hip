@@ -1058,6 +1058,9 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // catchments) measured 10 % slower than 32768 or 16384 (A/B, same box)
   while (h->max_blocks & (h->max_blocks - 1)) h->max_blocks &= h->max_blocks - 1;
   if (const char* e = std::getenv("TFG_BLOCKS")) h->max_blocks = std::max(1, atoi(e));
+  // no more workgroups (slab rows) than the grid has chunks: a one-cell BMI
+  // handle keeps one row, not 32768 (NextGen may hold thousands of handles)
+  h->max_blocks = (int)std::min<int64_t>(h->max_blocks, (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);
   if (const char* e = std::getenv("TFG_FUSE")) h->fuse = std::max(1, atoi(e));
   if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "stream create failed"; return bail(TFG_ERR_HIP); }
   h->stream = h->own_stream;
