@@ -214,14 +214,15 @@ def main():
     mean_launch_s = float(launch_ms.mean()) / 1e3
     bytes_launch = cells * (BYTES_PER_STEP * args.fuse + BYTES_PER_LAUNCH)
     achieved = bytes_launch / mean_launch_s / 1e9
-    pcie = pcie_inclusive(eng, args, torch) if rank == 0 and not args.no_pcie else None
+    # the host-fed leg and the CPU baseline run on rank 0 at N=1 only (BASELINE contract)
+    pcie = pcie_inclusive(eng, args, torch) if world == 1 and not args.no_pcie else None
     eng.close()
 
     result = None
     if rank == 0:
         cpu = None
         parity = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:
             # a short GPU run on the same sample cells for a parity spot check
             n = min(args.cpu_cells, cells)
             scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n, dt=args.dt))

@@ -6,7 +6,9 @@
 // + six outputs).  Reports GB/s for several (R, W) mixes so the measured
 // k_fused rate can be placed against what this read/write mix can reach.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
-//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048]
+//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0]
+// skew: extra cells between consecutive planes (plane stride = cells + skew),
+// to test whether power-of-two plane strides cost HBM channel balance.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -28,26 +30,27 @@ __device__ __forceinline__ void splat(float4& o, float a) { o = make_float4(a, a
 // V floats (V adjacent cells) per lane per plane; NT: non-temporal stores
 template <int R, int W, int V, bool NT = false>
 __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
-                                             int steps, int frames) {
+                                             int steps, int frames, uint32_t ps) {
   using T = typename Vec<V>::T;
   const uint32_t nv = n / V;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += stride) {
     float acc = 0.0f;
     for (int s = 0; s < steps; ++s) {
-      const T* fin = reinterpret_cast<const T*>(in + (size_t)(s % frames) * R * n);
+      const float* fin = in + (size_t)(s % frames) * R * ps;
       T v[R > 0 ? R : 1];
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[r] = fin[(size_t)r * nv + i];
+      for (int r = 0; r < R; ++r) v[r] = reinterpret_cast<const T*>(fin + (size_t)r * ps)[i];
 #pragma unroll
       for (int r = 0; r < R; ++r) acc += hsum(v[r]);
-      T* fo = reinterpret_cast<T*>(out + (size_t)(s % frames) * W * n);
+      float* fo = out + (size_t)(s % frames) * W * ps;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         T o;
         splat(o, acc + (float)w);
-        if constexpr (NT) __builtin_nontemporal_store(o, &fo[(size_t)w * nv + i]);
-        else fo[(size_t)w * nv + i] = o;
+        T* dst = reinterpret_cast<T*>(fo + (size_t)w * ps) + i;
+        if constexpr (NT) __builtin_nontemporal_store(o, dst);
+        else *dst = o;
       }
     }
     if (W == 0 && acc == -1.0f) out[i] = acc;  // keep the reads alive
@@ -55,6 +58,7 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float
 }
 
 static int g_blocks = 256 * 8;
+static uint32_t g_skew = 0;
 
 template <int R, int W, int V = 1, bool NT = false>
 void run(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
@@ -62,13 +66,14 @@ void run(const char* name, float* in, float* out, uint32_t n, int steps, int fra
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
   const int blocks = g_blocks;
-  k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  const uint32_t ps = n + g_skew;
+  k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames, ps);  // warm-up
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
     CHECK(hipEventRecord(a));
-    k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames);
+    k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames, ps);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms;
@@ -76,8 +81,8 @@ void run(const char* name, float* in, float* out, uint32_t n, int steps, int fra
     if (ms < best) best = ms;
   }
   const double bytes = (double)n * steps * 4.0 * (R + W);
-  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"bytes_per_lane\": %d, \"blocks\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
-              name, R, W, 4 * V, g_blocks, bytes / (best * 1e-3) / 1e9, best);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"bytes_per_lane\": %d, \"blocks\": %d, \"skew\": %u, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, 4 * V, g_blocks, g_skew, bytes / (best * 1e-3) / 1e9, best);
   CHECK(hipEventDestroy(a));
   CHECK(hipEventDestroy(b));
 }
@@ -86,12 +91,14 @@ int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
   if (argc > 3) g_blocks = std::atoi(argv[3]);
+  if (argc > 4) g_skew = (uint32_t)std::strtoul(argv[4], nullptr, 10);
+  if (g_skew % 4) { std::fprintf(stderr, "skew must be a multiple of 4 cells\n"); return 1; }
   const int frames = steps;  // one distinct frame per step, as k_fused (no address is touched twice)
   float *in, *out;
-  CHECK(hipMalloc(&in, (size_t)n * 4 * 7 * frames));
-  CHECK(hipMalloc(&out, (size_t)n * 4 * 7 * frames));
-  CHECK(hipMemset(in, 0, (size_t)n * 4 * 7 * frames));
-  CHECK(hipMemset(out, 0, (size_t)n * 4 * 7 * frames));
+  CHECK(hipMalloc(&in, (size_t)(n + g_skew) * 4 * 7 * frames));
+  CHECK(hipMalloc(&out, (size_t)(n + g_skew) * 4 * 7 * frames));
+  CHECK(hipMemset(in, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
+  CHECK(hipMemset(out, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
   run<6, 7>("k_fused step mix (6 read, 7 write)", in, out, n, steps, frames);
   run<6, 7, 1, true>("k_fused step mix, non-temporal stores", in, out, n, steps, frames);
   run<7, 0>("read only (7 planes)", in, out, n, steps, frames);
