@@ -1033,7 +1033,6 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->nx = nx;
   h->n = ny * nx;
   h->n_pad = round_up(h->n, 64);
-  if (const char* e = std::getenv("TFG_PLANE_SKEW")) h->n_pad += round_up(std::max(0, atoi(e)), 64);
   if (h->n_pad * 8 >= (int64_t)1 << 32) {
     h->err = "shard too large: ny*nx must stay below 2^29 cells per device (32-bit field offsets)";
     g_err = h->err;
