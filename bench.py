@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=20251001)
-    ap.add_argument("--cpu-cells", type=int, default=393216, help="cells in the CPU-baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=24)
+    ap.add_argument("--cpu-cells", type=int, default=1048576, help="cells in the C CPU-baseline sample")
+    ap.add_argument("--cpu-steps", type=int, default=96)
+    ap.add_argument("--numpy-cells", type=int, default=393216, help="cells in the numpy (1 core) sample, 24 steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-fed forcing) leg")
     ap.add_argument("--dt", type=float, default=1.0, help="time step [h] (BASELINE config 5: 0.25)")
@@ -70,11 +71,32 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, gpu_sample):
-    """Oracle (numpy fp64 restatement of the reference, 1 core) on the first
-    cells of rank 0's shard, same fp32 inputs; also a parity spot check."""
+def _cpu_threads() -> int:
+    """Host threads for the C baseline: the process's CPU share (16 on a one-GPU
+    box, where OMP_NUM_THREADS is set to it), never the whole machine."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    n = int(env) if env and env.isdigit() else avail
+    return max(1, min(n, avail, 16))
+
+
+def _floored_rel(g, r):
+    s_v = np.percentile(np.abs(r), 99)
+    fl = np.maximum(np.maximum(np.abs(r), s_v), 1e-300)
+    e = np.abs(g - r) / fl
+    return float(np.max(e)), float(np.mean(e > 1e-5))
+
+
+def cpu_baseline(args, run_gpu_sample):
+    """CPU legs on rank 0 at N=1, on the first cells of the shard, same fp32 inputs:
+    (1) the C oracle (oracle/tfg_oracle_c.c, fp64, OpenMP over the process's CPU
+        share) on --cpu-cells x --cpu-steps: the reported cpu_baseline;
+    (2) the numpy oracle (oracle/tfg_oracle.py, fp64, one core) on the first
+        --numpy-cells x 24 steps, reported beside it;
+    plus a parity spot check of the GPU on the C sample's cells and steps."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import tfg_oracle as O
+    import tfg_oracle_c as OC
 
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
@@ -82,26 +104,39 @@ def cpu_baseline(args, gpu_sample):
     steps = args.cpu_steps
     syn = synthetic_cells(args.seed, np.arange(n), diurnal_table(args.frames))
     frames = np.arange(steps) % args.frames
-    forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
     static = dict(elev=syn["elev"], slope=syn["slope"], aspect=syn["aspect"], h0_snow=syn["h_snow"],
                   h0_ice=syn["h_ice"], h0_swe=syn["h_swe"], h0_iwe=syn["h_iwe"])
     static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
     cfg = dict(BASE_CFG, dt=args.dt)
     clock = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
+    # (1) C oracle, all threads of this process's share
+    threads = _cpu_threads()
+    forcing = {k: np.ascontiguousarray(syn[k], dtype=np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
     t0 = time.perf_counter()
-    out, _ = O.run_oracle(cfg, static, forcing, steps, clock=(clock[0], clock[3]))
-    dt = time.perf_counter() - t0
+    out, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(clock[0], clock[3]), frames=frames, hist=False,
+                             nthreads=threads)
+    t_c = time.perf_counter() - t0
+    cpu = {"value": n * steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/tfg_oracle_c.c (C fp64 restatement of update(), OpenMP, {threads} threads) on the "
+                     f"first {n} cells x {steps} hourly steps of the same synthetic workload ({t_c:.1f} s)"}
     parity = None
-    if gpu_sample is not None:
-        errs = []
-        for name, g in gpu_sample.items():
-            r = out[name][-1][: g.size]
-            s_v = np.percentile(np.abs(r), 99)
-            errs.append(float(np.max(np.abs(g - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300))))
-        parity = max(errs)
-    return {"value": n * steps / dt, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/tfg_oracle.py (numpy fp64 restatement of update(), single thread) on the first "
-                      f"{n} cells x {steps} hourly steps of the same synthetic workload ({dt:.1f} s)"}, parity
+    gpu = run_gpu_sample(n, steps)
+    if gpu is not None:
+        errs = {k: _floored_rel(g, out[k]) for k, g in gpu.items()}
+        parity = {"vs": "C oracle", "cells": n, "steps": steps,
+                  "max_floored_rel": max(e[0] for e in errs.values()),
+                  "frac_above_1e-5": {k: e[1] for k, e in errs.items()}}
+    # (2) numpy oracle, one core
+    m = min(args.numpy_cells, n)
+    fnp = {k: syn[k][frames[:24], :m].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    snp = {k: v[:m] for k, v in static.items()}
+    t0 = time.perf_counter()
+    O.run_oracle(cfg, snp, fnp, min(24, steps), clock=(clock[0], clock[3]))
+    t_np = time.perf_counter() - t0
+    numpy_leg = {"value": m * min(24, steps) / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+                 "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on the first {m} cells x "
+                           f"{min(24, steps)} hourly steps ({t_np:.1f} s)"}
+    return cpu, numpy_leg, parity
 
 
 def catchment_blocks(row0, rows, ny_global, nx, k):
@@ -210,7 +245,6 @@ def main():
     value = total_cells * steps / elapsed
     diag = allreduce_diagnostics(eng.diagnostics()) if world > 1 else eng.diagnostics()
 
-    gpu_sample = None
     mean_launch_s = float(launch_ms.mean()) / 1e3
     bytes_launch = cells * (BYTES_PER_STEP * args.fuse + BYTES_PER_LAUNCH)
     achieved = bytes_launch / mean_launch_s / 1e9
@@ -220,20 +254,22 @@ def main():
 
     result = None
     if rank == 0:
-        cpu = None
-        parity = None
+        cpu = numpy_leg = parity = None
         if world == 1 and not args.no_cpu_baseline:
-            # a short GPU run on the same sample cells for a parity spot check
-            n = min(args.cpu_cells, cells)
-            scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n, dt=args.dt))
-            se = GlacierEngine(scfg, 1, n, engine=args.engine, device=local, n_frames=args.frames,
-                               hist_depth=1, fuse_steps=args.fuse)
-            se.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=n)
-            se.run(args.cpu_steps)
-            se.sync()
-            gpu_sample = {k: se.get_field(k) for k in ("M_total", "SM", "IM", "RH", "h_snow")}
-            se.close()
-            cpu, parity = cpu_baseline(args, gpu_sample)
+            def run_gpu_sample(n, steps):
+                # the GPU engine on the CPU sample's cells and steps (a parity spot check)
+                scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n, dt=args.dt))
+                se = GlacierEngine(scfg, 1, n, engine=args.engine, device=local, n_frames=args.frames,
+                                   hist_depth=1, fuse_steps=args.fuse)
+                try:
+                    se.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=n)
+                    se.run(steps)
+                    se.sync()
+                    return {k: se.get_field(k) for k in ("M_total", "SM", "IM", "RH", "h_snow")}
+                finally:
+                    se.close()
+
+            cpu, numpy_leg, parity = cpu_baseline(args, run_gpu_sample)
         traffic = None
         pmc = ROOT / "profiles" / f"pmc_{args.nx}x{args.ny}_fuse{args.fuse}.json"
         if pmc.exists():
@@ -271,8 +307,9 @@ def main():
                 "kernel_ms_per_launch": float(launch_ms.mean()),
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_numpy_1core": numpy_leg,
             "pcie_inclusive": pcie,
-            "sample_parity_floored_rel": parity,
+            "sample_parity": parity,
             "mass_balance": {k: float(v) for k, v in zip(["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"], diag[0])},
         }
         print(json.dumps(result), flush=True)
