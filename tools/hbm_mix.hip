@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); std::exit(1); } } while (0)
@@ -57,6 +58,30 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float
   }
 }
 
+// Block-interleaved layout: within a frame, cell i of plane r sits at
+// ((i / IL) * P + r) * IL + i % IL (P planes), so one wave's P accesses of a
+// step fall in one contiguous P*IL*4-byte run instead of P separate planes.
+template <int R, int W, int IL>
+__global__ __launch_bounds__(256) void k_mix_il(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
+                                                int steps, int frames) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t blk = i / IL, off = i % IL;
+    float acc = 0.0f;
+    for (int s = 0; s < steps; ++s) {
+      const float* fin = in + (size_t)(s % frames) * R * n + (size_t)blk * R * IL + off;
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = fin[r * IL];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc += v[r];
+      float* fo = out + (size_t)(s % frames) * W * n + (size_t)blk * W * IL + off;
+#pragma unroll
+      for (int w = 0; w < W; ++w) fo[w * IL] = acc + (float)w;
+    }
+  }
+}
+
 static int g_blocks = 256 * 8;
 static uint32_t g_skew = 0;
 
@@ -87,6 +112,31 @@ void run(const char* name, float* in, float* out, uint32_t n, int steps, int fra
   CHECK(hipEventDestroy(b));
 }
 
+template <int R, int W, int IL>
+void run_il(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  k_mix_il<R, W, IL><<<g_blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    CHECK(hipEventRecord(a));
+    k_mix_il<R, W, IL><<<g_blocks, 256>>>(in, out, n, steps, frames);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  const double bytes = (double)n * steps * 4.0 * (R + W);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"interleave_cells\": %d, \"blocks\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, IL, g_blocks, bytes / (best * 1e-3) / 1e9, best);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
@@ -99,6 +149,17 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(in, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(out, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
+  if (argc > 5 && std::string(argv[5]) == "il") {  // layout experiment only
+    run<6, 7>("k_fused step mix (6 read, 7 write), planar", in, out, n, steps, frames);
+    run_il<6, 7, 64>("k_fused step mix, 64-cell block interleave", in, out, n, steps, frames);
+    run_il<6, 7, 256>("k_fused step mix, 256-cell block interleave", in, out, n, steps, frames);
+    run_il<6, 7, 1024>("k_fused step mix, 1024-cell block interleave", in, out, n, steps, frames);
+    run<6, 7>("k_fused step mix (6 read, 7 write), planar", in, out, n, steps, frames);
+    run_il<6, 7, 64>("k_fused step mix, 64-cell block interleave", in, out, n, steps, frames);
+    CHECK(hipFree(in));
+    CHECK(hipFree(out));
+    return 0;
+  }
   run<6, 7>("k_fused step mix (6 read, 7 write)", in, out, n, steps, frames);
   run<6, 7, 1, true>("k_fused step mix, non-temporal stores", in, out, n, steps, frames);
   run<7, 0>("read only (7 planes)", in, out, n, steps, frames);
