@@ -98,14 +98,22 @@ MELT_OUT_EPS = 1e-9  # m of snow depth: "melt-out" vicinity for the residual-fli
 def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
     """Cells whose trajectories part at a melt-out residual.
 
-    The reference decides ice melt with ``h_swe == 0 & previous_swe == 0``
-    (bmi_topoflow_glacier.py:1424) on h_swe = max(h - (h/3600)*dt*3600, 0),
-    whose sub-ulp residual is 0 or ~1e-19 depending on the last bit of h.
-    Any engine whose state differs from the reference in the last bit can land
-    on the other side, which switches IM on one step earlier or later.
-    A cell is classified as a flip at step k when (a) it is the cell's first
-    step outside tolerance, (b) the IM on/off gate differs there, and (c) one
-    trajectory has a snow depth within MELT_OUT_EPS of zero at k or k-1.
+    The reference tests float state for exact zero in three places:
+    ``h_swe == 0 & previous_swe == 0`` gates ice melt (bmi_topoflow_glacier.py:1424),
+    ``h_snow == 0`` resets the snowpack cold content (:1562), and ``h_ice == 0``
+    resets the ice cold content (:1426).  The depths come from
+    h = max(h - (h/3600)*dt*3600, 0), whose sub-ulp residual is 0 or ~1e-19
+    depending on the last bit of h, so any engine whose state differs from the
+    reference in the last bit can land on the other side of a gate.  Through
+    IM that switches ice melt on a step earlier or later; through the reset
+    cold content it moves the next melt onset of a thin new snowpack by a step.
+    A cell is classified as a flip at step k, its first step outside tolerance,
+    when either
+      (a) the IM on/off gate differs at k and one trajectory has a snow depth
+          within MELT_OUT_EPS of zero at k or k-1, or
+      (b) at some step j <= k exactly one trajectory has a snow (or ice) depth
+          of exactly zero and the other a residual within MELT_OUT_EPS: the
+          zero gates have diverged while every output was still in tolerance.
     Returns (flip_step per cell or -1, list of genuinely failing (cell, step, var)).
     """
     names = [v for v in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") if v in gpu]
@@ -115,6 +123,15 @@ def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
         g, r = np.asarray(gpu[v], np.float64), np.asarray(ref[v], np.float64)
         fl = np.abs(g - r) / np.maximum(np.maximum(np.abs(r), scale_floor(r)), 1e-300)
         bad |= fl > rtol
+    # (b): first step at which the exact-zero status of a depth diverges at residual scale
+    split = np.full(ncell, nsteps)
+    for v in ("h_snow", "h_ice"):
+        if v not in gpu:
+            continue
+        g, r = np.abs(np.asarray(gpu[v], np.float64)), np.abs(np.asarray(ref[v], np.float64))
+        d = ((g == 0) != (r == 0)) & (np.maximum(g, r) <= MELT_OUT_EPS)
+        first = np.where(d.any(axis=0), np.argmax(d, axis=0), nsteps)
+        split = np.minimum(split, first)
     flip = np.full(ncell, -1)
     genuine = []
     for c in np.nonzero(bad.any(axis=0))[0]:
@@ -122,7 +139,7 @@ def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
         gate = (np.asarray(gpu["IM"])[k, c] > 0) != (np.asarray(ref["IM"])[k, c] > 0)
         ks = [k] + ([k - 1] if k > 0 else [])
         near = min(min(abs(float(np.asarray(gpu["h_snow"])[j, c])), abs(float(np.asarray(ref["h_snow"])[j, c]))) for j in ks)
-        if gate and near <= MELT_OUT_EPS:
+        if (gate and near <= MELT_OUT_EPS) or split[c] <= k:
             flip[c] = k
         else:
             genuine.append((int(c), k, [v for v in names if np.abs(np.asarray(gpu[v])[k, c] - np.asarray(ref[v])[k, c])
