@@ -3,7 +3,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${PMC_TAG:-pmc}
 mkdir -p $OUT
-ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --steps 48 --warmup 24 --no-cpu-baseline}"
+ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --steps 48 --warmup 24 --no-cpu-baseline --no-pcie}"
 i=0
 while IFS= read -r line; do
   [ -z "$line" ] && continue
