@@ -90,11 +90,17 @@ class GlacierEngine:
         """Copy a host array (broadcast to n cells) or a torch CUDA tensor into a field."""
         fid = nat.FIELD[name]
         if hasattr(values, "data_ptr") and getattr(values, "is_cuda", False):
+            import torch
+
             t = values.contiguous()
             code = {4: nat.F32, 8: nat.F64}[t.element_size()] if name != "catch_id" else nat.I32
             if t.numel() != self.n:
                 raise ValueError(f"{name}: {t.numel()} values for {self.n} cells")
+            # the engine copies on its own stream: wait for torch's producer
+            # first, and for the copy before `t` (maybe a temporary) is freed
+            torch.cuda.current_stream(t.device).synchronize()
             self._chk(self.lib.tfg_set_field(self.h, fid, index, ctypes.c_void_p(t.data_ptr()), code, self.n, 1))
+            self.sync()
             return
         if name == "catch_id":
             a = np.ascontiguousarray(np.broadcast_to(np.asarray(values, dtype=np.int32), (self.n,)))
@@ -117,6 +123,24 @@ class GlacierEngine:
             out = np.empty(self.n, dtype=dtype)
             code = nat.F32 if out.dtype == np.float32 else nat.F64
         self._chk(self.lib.tfg_get_field(self.h, fid, index, out.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
+        return out
+
+    def get_field_device(self, name: str, out, index: int | None = None):
+        """Copy a field into the torch CUDA tensor `out` (n elements; float32,
+        float64, or int32 for catch_id).  tfg_get_field with a device pointer
+        is asynchronous on the engine's stream, so this waits for the copy
+        before torch's stream may read `out`."""
+        import torch
+
+        fid = nat.FIELD[name]
+        if index is None:
+            index = self.last_hist if name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") else 0
+        if not (out.is_cuda and out.is_contiguous() and out.numel() == self.n):
+            raise ValueError(f"{name}: need a contiguous CUDA tensor of {self.n} elements")
+        code = {torch.float32: nat.F32, torch.float64: nat.F64, torch.int32: nat.I32}[out.dtype]
+        torch.cuda.current_stream(out.device).synchronize()  # `out` may still be in use on torch's stream
+        self._chk(self.lib.tfg_get_field(self.h, fid, index, ctypes.c_void_p(out.data_ptr()), code, self.n, 1))
+        self.sync()
         return out
 
     def set_inputs(self, values: np.ndarray, index: int = 0) -> None:
@@ -247,6 +271,11 @@ class GlacierEngine:
                 raise ValueError(f"halo rows need nx = {self.nx} values")
         if on_dev and any(isinstance(k, np.ndarray) for k in keep):
             raise ValueError("halo rows must be both host arrays or both device tensors")
+        if on_dev:
+            import torch
+
+            # RCCL receives complete on torch's stream; the engine reads on its own
+            torch.cuda.current_stream(keep[0].device).synchronize()
         self._chk(self.lib.tfg_terrain_from_dem(self.h, float(dx), float(dy), ptrs[0], ptrs[1], dtype, on_dev))
 
     # -- mass balance -------------------------------------------------------------
