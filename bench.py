@@ -61,7 +61,8 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=20251001)
     ap.add_argument("--cpu-cells", type=int, default=1048576, help="cells in the C CPU-baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=96)
+    ap.add_argument("--cpu-steps", type=int, default=768, help="steps of the C CPU-baseline sample (~10 s on 16 threads)")
+    ap.add_argument("--parity-steps", type=int, default=96, help="steps of the GPU-vs-C-oracle spot check")
     ap.add_argument("--parity-cells", type=int, default=262144, help="cells of the GPU-vs-C-oracle spot check")
     ap.add_argument("--numpy-cells", type=int, default=393216, help="cells in the numpy (1 core) sample, 24 steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -104,7 +105,7 @@ def cpu_baseline(args, run_gpu_sample):
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
     n = min(args.cpu_cells, args.nx * args.ny)
-    steps = args.cpu_steps
+    steps = max(args.cpu_steps, args.parity_steps)
     syn = synthetic_cells(args.seed, np.arange(n), diurnal_table(args.frames))
     frames = np.arange(steps) % args.frames
     static = dict(elev=syn["elev"], slope=syn["slope"], aspect=syn["aspect"], h0_snow=syn["h_snow"],
@@ -116,15 +117,16 @@ def cpu_baseline(args, run_gpu_sample):
     threads = _cpu_threads()
     forcing = {k: np.ascontiguousarray(syn[k], dtype=np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
     t0 = time.perf_counter()
-    out, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(clock[0], clock[3]), frames=frames, hist=False,
-                             nthreads=threads)
+    out, _ = OC.run_oracle_c(cfg, static, forcing, args.cpu_steps, clock=(clock[0][:args.cpu_steps], clock[3][:args.cpu_steps]),
+                             frames=frames[:args.cpu_steps], hist=False, nthreads=threads)
     t_c = time.perf_counter() - t0
-    cpu = {"value": n * steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
+    cpu = {"value": n * args.cpu_steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
            "sample": f"oracle/tfg_oracle_c.c (C fp64 restatement of update(), OpenMP, {threads} threads) on the "
-                     f"first {n} cells x {steps} hourly steps of the same synthetic workload ({t_c:.1f} s)"}
+                     f"first {n} cells x {args.cpu_steps} hourly steps of the same synthetic workload ({t_c:.1f} s)"}
     parity = None
     pn = min(args.parity_cells, n)
-    gpu = run_gpu_sample(pn, steps)
+    ps = args.parity_steps
+    gpu = run_gpu_sample(pn, ps)
     if gpu is not None:
         # every step of the first pn cells, GPU history vs the C oracle; cells whose
         # trajectories part at a melt-out residual (DESIGN.md "Melt-out flips") are
@@ -132,11 +134,11 @@ def cpu_baseline(args, run_gpu_sample):
         from tests.harness import melt_out_flips, valid_mask
 
         ref, _ = OC.run_oracle_c(cfg, {k: v[:pn] for k, v in static.items()},
-                                 {k: np.ascontiguousarray(v[:, :pn]) for k, v in forcing.items()}, steps,
-                                 clock=(clock[0], clock[3]), frames=frames, hist=True, nthreads=threads)
+                                 {k: np.ascontiguousarray(v[:, :pn]) for k, v in forcing.items()}, ps,
+                                 clock=(clock[0][:ps], clock[3][:ps]), frames=frames[:ps], hist=True, nthreads=threads)
         flip, genuine = melt_out_flips(gpu, ref)
-        ok = valid_mask(flip, steps)
-        parity = {"vs": "C oracle", "cells": pn, "steps": steps, "outputs": sorted(gpu),
+        ok = valid_mask(flip, ps)
+        parity = {"vs": "C oracle", "cells": pn, "steps": ps, "outputs": sorted(gpu),
                   "max_floored_rel": max(_floored_rel(g[ok], ref[k][ok])[0] for k, g in gpu.items()),
                   "tolerance": 1e-5, "melt_out_flips": int((flip >= 0).sum()), "genuine_mismatches": len(genuine)}
     # (2) numpy oracle, one core

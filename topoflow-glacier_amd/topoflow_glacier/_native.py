@@ -75,6 +75,17 @@ def load() -> ctypes.CDLL:
             "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
             "There is no CPU fallback."
         )
+    # One HIP runtime per process.  The torch wheel bundles its own
+    # libamdhip64 under the same soname as /opt/rocm's; if this library were
+    # loaded first it would bind /opt/rocm's runtime, and a later
+    # `import torch` would load a second runtime that then reports no GPU.
+    # Importing torch first makes this library bind torch's runtime, which
+    # every caller that also uses torch (bench, sharding, device-tensor I/O)
+    # then shares.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(str(LIB_PATH))
     vp, i64, i32, dp = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
     sigs = {
