@@ -59,3 +59,30 @@ if cells:
                 print(f"    {v:8s} gpu {gpu[v][j, c]: .9e}  C {ref[v][j, c]: .9e}  numpy {npo[v][j, i]: .9e}")
         for v in ("albedo", "n", "Eccs", "Ecci", "Q_sum", "Qn_SW"):
             print(f"    numpy {v:6s} " + " ".join(f"{npo[v][j, i]: .6e}" for j in range(max(0, k - 3), min(steps, k + 2))))
+
+# Where does the largest in-tolerance error sit?  Per variable: the max
+# floored error over unflipped (cell, step) pairs and the worst cell's trace.
+from tests.harness import valid_mask  # noqa: E402
+
+ok = valid_mask(flip, steps)
+worst = []
+for v in names:
+    r, g = ref[v], gpu[v]
+    nz = np.abs(r[r != 0])
+    s_v = np.percentile(nz, 99) if nz.size else 0.0
+    e = np.where(ok, np.abs(g - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300), 0.0)
+    k, c = np.unravel_index(np.argmax(e), e.shape)
+    print(f"{v:8s} max floored err {e.max():.3e} at cell {c} step {k}; s_v {s_v:.3e}; "
+          f"frac > 1e-6: {np.mean(e > 1e-6):.2e}")
+    worst.append((e.max(), v, int(c), int(k)))
+worst.sort(reverse=True)
+cells = sorted({c for _, _, c, _ in worst[:3]})
+sub = {kk: v[cells] for kk, v in static.items()}
+fnp = {kk: syn[kk][frames][:, cells].astype(np.float64) for kk in forcing}
+npo, _ = O.run_oracle(cfg, sub, fnp, steps, clock=(clock[0], clock[3]))
+for err, v, c, k in worst[:3]:
+    i = cells.index(c)
+    print(f"\nworst {v} cell {c} step {k} err {err:.3e}")
+    for j in range(max(0, k - 4), min(steps, k + 2)):
+        print(f"  step {j}: {v} gpu {gpu[v][j, c]: .9e} ref {ref[v][j, c]: .9e}; numpy Eccs {npo['Eccs'][j, i]: .6e} "
+              f"Ecci {npo['Ecci'][j, i]: .6e} Q_sum {npo['Q_sum'][j, i]: .6e} h_swe {npo['h_swe'][j, i]: .6e}")
