@@ -6,7 +6,7 @@
 // + six outputs).  Reports GB/s for several (R, W) mixes so the measured
 // k_fused rate can be placed against what this read/write mix can reach.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
-//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0]
+//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0] [il|pf]
 // skew: extra cells between consecutive planes (plane stride = cells + skew),
 // to test whether power-of-two plane strides cost HBM channel balance.
 #include <hip/hip_runtime.h>
@@ -137,6 +137,65 @@ void run_il(const char* name, float* in, float* out, uint32_t n, int steps, int 
   CHECK(hipEventDestroy(b));
 }
 
+
+// Software-pipelined variant: each thread keeps D steps of reads in flight
+// (register ring, loads of step s+D issued before step s is consumed), the
+// k_fused structure with a deeper read-ahead.  Requires steps % D == 0.
+template <int R, int W, int D, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void k_mix_pf(const float* __restrict__ in, float* __restrict__ out,
+                                                       uint32_t n, int steps, int frames) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float buf[D][R > 0 ? R : 1];
+    auto fetch = [&](int s, float (&b)[R > 0 ? R : 1]) {
+      const int ss = s < steps ? s : steps - 1;
+      const float* fin = in + (size_t)(ss % frames) * R * n + i;
+#pragma unroll
+      for (int r = 0; r < R; ++r) b[r] = __builtin_nontemporal_load(fin + (size_t)r * n);
+    };
+#pragma unroll
+    for (int j = 0; j < D; ++j) fetch(j, buf[j]);
+    float acc = 0.0f;
+    for (int s0 = 0; s0 < steps; s0 += D) {
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc += buf[j][r];
+        fetch(s0 + j + D, buf[j]);
+        float* fo = out + (size_t)((s0 + j) % frames) * W * n + i;
+#pragma unroll
+        for (int w = 0; w < W; ++w) __builtin_nontemporal_store(acc + (float)w, fo + (size_t)w * n);
+      }
+    }
+    if (W == 0 && acc == -1.0f) out[i] = acc;  // keep the reads alive
+  }
+}
+
+template <int R, int W, int D, int WAVES>
+void run_pf(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  k_mix_pf<R, W, D, WAVES><<<g_blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    CHECK(hipEventRecord(a));
+    k_mix_pf<R, W, D, WAVES><<<g_blocks, 256>>>(in, out, n, steps, frames);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  const double bytes = (double)n * steps * 4.0 * (R + W);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"prefetch_steps\": %d, \"min_waves_per_simd\": %d, \"blocks\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, D, WAVES, g_blocks, bytes / (best * 1e-3) / 1e9, best);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
@@ -149,6 +208,20 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(in, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(out, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
+  if (argc > 5 && std::string(argv[5]) == "pf") {  // read-ahead depth experiment only
+    run<6, 7, 1, true>("k_fused step mix, plain loop, nt stores", in, out, n, steps, frames);
+    run_pf<6, 7, 1, 4>("k_fused step mix, read-ahead 1", in, out, n, steps, frames);
+    run_pf<6, 7, 2, 4>("k_fused step mix, read-ahead 2", in, out, n, steps, frames);
+    run_pf<6, 7, 4, 4>("k_fused step mix, read-ahead 4", in, out, n, steps, frames);
+    run_pf<6, 7, 4, 2>("k_fused step mix, read-ahead 4, 2 waves/SIMD bound", in, out, n, steps, frames);
+    run_pf<6, 7, 8, 2>("k_fused step mix, read-ahead 8, 2 waves/SIMD bound", in, out, n, steps, frames);
+    run_pf<7, 0, 1, 4>("read only, read-ahead 1", in, out, n, steps, frames);
+    run_pf<7, 0, 4, 4>("read only, read-ahead 4", in, out, n, steps, frames);
+    run_pf<1, 1, 4, 4>("copy, read-ahead 4", in, out, n, steps, frames);
+    CHECK(hipFree(in));
+    CHECK(hipFree(out));
+    return 0;
+  }
   if (argc > 5 && std::string(argv[5]) == "il") {  // layout experiment only
     run<6, 7>("k_fused step mix (6 read, 7 write), planar", in, out, n, steps, frames);
     run_il<6, 7, 64>("k_fused step mix, 64-cell block interleave", in, out, n, steps, frames);
