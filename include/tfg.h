@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 2
+#define TFG_ABI_VERSION 3
 
 /* status codes */
 enum {
@@ -105,6 +105,8 @@ typedef struct tfg_params {
   double sigma, sea_level_p0, uni_gas_const, M_mass_air, z0_air, em_surf;
   int32_t satterlund;    /* config.py:101                                      */
   int32_t ring_len;      /* int(3*24/dt) snowfall-window slots (:296)          */
+  double glens_A;        /* Glen's flow-law rate factor [Pa^-3 yr^-1] (config.py:65);
+                            read only by the optional ice-flow term          */
 } tfg_params;
 
 /* Per-step uniform scalars, computed on the host in fp64 from the model clock
@@ -254,6 +256,34 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
  * RCCL over xGMI); the sharded result equals the unsharded one. */
 int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_north, const void* halo_south,
                          int halo_dtype, int halo_on_device);
+
+/* Optional lateral ice flow (extension): the
+ * shallow-ice approximation with Glen's law (n = 3) moves ice thickness
+ * H = h_iwe * rho_H2O/rho_ice between neighbouring cells over the bed
+ * `elev`.  The reference declares the flow parameters (glens_A, in
+ * Pa^-3 yr^-1, config.py:64-65) but never moves ice (Qc = Qa = 0, :936-955),
+ * so the term is off unless a caller invokes it and results then depart from
+ * the reference by design.  Explicit, flux form on cell faces, fp64:
+ *   q_face = -Gamma * Hf^5 * |grad s|^2 * ds/dn,  Gamma = 2A/5 (rho_ice g)^3,
+ *   Hf the face-mean thickness, each face flux limited to a quarter of the
+ *   donor cell's ice per sub-step (H never goes negative), zero flux across
+ *   the domain edge.  Ice volume is conserved to rounding.
+ * Halo rows are [2][nx] fp64: row 0 the surface elevation s = elev + H, row 1
+ * the ice thickness H, of the neighbour shard's row adjacent to this shard;
+ * NULL at the domain edge.  Row-block shards exchange them before every
+ * sub-step (topoflow_glacier/sharding.py, RCCL over xGMI); the sharded result
+ * equals the unsharded one bit for bit.
+ *
+ * This shard's first and last rows as halo rows for its neighbours
+ * (first[2][nx], last[2][nx], fp64; blocking). */
+int tfg_ice_flow_edges(tfg_handle* h, double* first, double* last, int on_device);
+/* Largest face diffusivity Gamma*Hf^5*|grad s|^2 [m2 yr-1] (blocking); it
+ * sets the stable sub-step dt <= min(dx, dy)^2 / (4 D). */
+int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_north, const double* halo_south,
+                      int halo_on_device, double* dmax);
+/* One explicit sub-step of dt_years. */
+int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
+                      const double* halo_south, int halo_on_device);
 
 /* Last error message of a handle (NULL: the last create/global error). */
 const char* tfg_last_error(const tfg_handle* h);

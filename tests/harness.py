@@ -305,3 +305,103 @@ def terrain_oracle(dem: np.ndarray, dx: float, dy: float, north=None, south=None
 
 def ns(**kw):
     return SimpleNamespace(**kw)
+
+
+# ---------------------------------------------------------------- optional ice flow (tfg_ice_flow_*)
+def ice_flow_gamma(cfg: dict) -> float:
+    """Gamma = 2A/5 (rho_ice g)^3 for Glen's law n = 3, as tfg_create folds it."""
+    c = cfg_object(cfg)
+    rg = c.rho_ice * c.g
+    return 2.0 * c.glens_A / 5.0 * (rg * rg * rg)
+
+
+def _flow_faces(elev, iwe, wi, gamma, dx, dy, north, south):
+    """Face normal/tangential gradients and thicknesses of one shard (numpy
+    restatement of k_ice_flow's flow_grad_x / flow_grad_y, same op order)."""
+    iwe = np.asarray(iwe, np.float64)
+    H = iwe * wi
+    S = np.asarray(elev, np.float64) + iwe * wi
+    Sn = S[0] if north is None else np.asarray(north[0], np.float64)
+    Ss = S[-1] if south is None else np.asarray(south[0], np.float64)
+    Hn = H[0] if north is None else np.asarray(north[1], np.float64)
+    Hs = H[-1] if south is None else np.asarray(south[1], np.float64)
+    P = np.vstack([Sn[None], S, Ss[None]])
+    P = np.hstack([P[:, :1], P, P[:, -1:]])  # rows -1..ny, columns -1..nx (edge replicated)
+    Hp = np.vstack([Hn[None], H, Hs[None]])
+    gnx = (P[1:-1, 2:-1] - P[1:-1, 1:-2]) / dx
+    gtx = ((P[2:, 1:-2] - P[:-2, 1:-2]) + (P[2:, 2:-1] - P[:-2, 2:-1])) / (4.0 * dy)
+    gny = (P[1:, 1:-1] - P[:-1, 1:-1]) / dy
+    gty = ((P[:-1, 2:] - P[:-1, :-2]) + (P[1:, 2:] - P[1:, :-2])) / (4.0 * dx)
+    return H, Hp, gnx, gtx, gny, gty
+
+
+def _face_D(Ha, Hb, gn, gt, gamma):
+    Hf = 0.5 * (Ha + Hb)
+    h2 = Hf * Hf
+    h5 = (h2 * h2) * Hf
+    return (gamma * h5) * (gn * gn + gt * gt)
+
+
+def _face_q(Ha, Hb, gn, gt, gamma, dn, dt):
+    q = -(_face_D(Ha, Hb, gn, gt, gamma) * gn)
+    Hd = np.where(q > 0.0, Ha, Hb)
+    qlim = (Hd * dn) / (4.0 * dt)
+    return np.minimum(np.maximum(q, -qlim), qlim)
+
+
+def ice_flow_step_restated(elev, iwe, wi, gamma, dx, dy, dt, north=None, south=None):
+    """One explicit shallow-ice sub-step of a [ny][nx] shard: the numpy
+    restatement tfg_ice_flow_step is checked against (test infrastructure)."""
+    H, Hp, gnx, gtx, gny, gty = _flow_faces(elev, iwe, wi, gamma, dx, dy, north, south)
+    ny, nx = H.shape
+    qx = _face_q(H[:, :-1], H[:, 1:], gnx, gtx, gamma, dx, dt)  # faces (r, c+1/2)
+    qy = _face_q(Hp[:-1], Hp[1:], gny, gty, gamma, dy, dt)     # faces (r+1/2, c), r = -1..ny-1
+    if north is None:
+        qy[0] = 0.0
+    if south is None:
+        qy[-1] = 0.0
+    z = np.zeros((ny, 1))
+    qE = np.hstack([qx, z])
+    qW = np.hstack([z, qx])
+    div = (qE - qW) / dx + (qy[1:] - qy[:-1]) / dy
+    return np.maximum(np.asarray(iwe, np.float64) - (dt / wi) * div, 0.0)
+
+
+def ice_flow_dmax_restated(elev, iwe, wi, gamma, dx, dy, north=None, south=None):
+    H, Hp, gnx, gtx, gny, gty = _flow_faces(elev, iwe, wi, gamma, dx, dy, north, south)
+    Dx = _face_D(H[:, :-1], H[:, 1:], gnx, gtx, gamma)
+    Dy = _face_D(Hp[:-1], Hp[1:], gny, gty, gamma)
+    lo, hi = (0 if north is not None else 1), (Dy.shape[0] if south is not None else Dy.shape[0] - 1)
+    return float(max(Dx.max(initial=0.0), Dy[lo:hi].max(initial=0.0)))
+
+
+class RestatedFlowShard:
+    """A CPU stand-in with GlacierEngine's ice_flow_* methods, backed by the
+    restatement: lets the sharded orchestration (sharding.ice_flow) run under
+    gloo on CPU.  Test infrastructure."""
+
+    def __init__(self, elev, iwe, wi, gamma):
+        self.elev = np.asarray(elev, np.float64)
+        self.iwe = np.asarray(iwe, np.float64).copy()
+        self.wi, self.gamma = wi, gamma
+        self.ny, self.nx = self.iwe.shape
+
+    def ice_flow_edges(self):
+        S = self.elev + self.iwe * self.wi
+        H = self.iwe * self.wi
+        return np.stack([S[0], H[0]]), np.stack([S[-1], H[-1]])
+
+    def ice_flow_dmax(self, dx, dy, north=None, south=None):
+        return ice_flow_dmax_restated(self.elev, self.iwe, self.wi, self.gamma, dx, dy, north, south)
+
+    def ice_flow_step(self, dt, dx, dy, north=None, south=None):
+        self.iwe = ice_flow_step_restated(self.elev, self.iwe, self.wi, self.gamma, dx, dy, dt, north, south)
+
+
+def glacier_valley(ny: int, nx: int, dx: float = 100.0):
+    """A bed tilted down-valley with a valley glacier on it: (bed [m] fp32-exact,
+    ice water equivalent h_iwe [m])."""
+    y, x = np.mgrid[0:ny, 0:nx].astype(np.float64)
+    bed = 3000.0 - 0.08 * dx * y + 0.002 * (x - nx / 2) ** 2 * dx
+    H = np.maximum(0.0, 220.0 * (1.0 - ((x - nx / 2) / (0.35 * nx)) ** 2 - ((y - 0.4 * ny) / (0.45 * ny)) ** 2))
+    return bed.astype(np.float32).astype(np.float64), H * (917.0 / 1000.0)

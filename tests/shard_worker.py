@@ -24,7 +24,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain"], required=True)
+    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain", "flow", "gpu_flow"], required=True)
     ap.add_argument("--ny", type=int, required=True)
     ap.add_argument("--nx", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
@@ -63,6 +63,29 @@ def main():
             np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, slope=eng.get_field("slope"),
                      aspect=eng.get_field("aspect"))
             eng.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    if a.mode in ("flow", "gpu_flow"):
+        # the optional ice-flow term over row blocks: sharding.ice_flow swaps
+        # the halo rows over gloo before every sub-step (--steps = years x 10)
+        from tests.harness import BASE_CFG, RestatedFlowShard, glacier_valley, ice_flow_gamma, make_engine
+        from topoflow_glacier.sharding import ice_flow
+
+        bed, iwe = glacier_valley(a.ny, a.nx)
+        blk = slice(row0, row0 + rows)
+        if a.mode == "flow":
+            sh = RestatedFlowShard(bed[blk], iwe[blk], 1000.0 / 917.0, ice_flow_gamma(BASE_CFG))
+        else:
+            sh = make_engine(dict(BASE_CFG), rows, a.nx, "float32", n_frames=1, hist_depth=1, row0=row0)
+            sh.set_field("elev", bed[blk].reshape(-1).astype(np.float32))
+            sh.set_field("h_iwe", iwe[blk].reshape(-1))
+            sh.init_state()
+        n_sub = ice_flow(sh, a.steps / 10.0, 100.0, 100.0)
+        out = sh.iwe.reshape(-1) if a.mode == "flow" else sh.get_field("h_iwe")
+        np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, iwe=out, n_sub=n_sub)
+        if a.mode == "gpu_flow":
+            sh.close()
         dist.barrier()
         dist.destroy_process_group()
         return

@@ -657,6 +657,154 @@ __global__ void k_terrain(const R* __restrict__ elev, const double* __restrict__
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Optional lateral ice flow (tfg_ice_flow_*): shallow-ice approximation,
+// Glen's law n = 3, explicit flux form on cell faces, fp64, contraction off so
+// the face flux two neighbours compute is the same number (exact
+// conservation, and sharded == unsharded bit for bit).  The reference declares
+// the parameters (glens_A, config.py:64-65) but moves no ice (:936-955).
+//   H = h_iwe * wi (ice thickness), s = elev + H (elev is the bed)
+//   q = -Gamma * Hf^5 * (gn^2 + gt^2) * gn on a face with normal gradient gn,
+//   tangential gradient gt (mean of the two cells' centred differences) and
+//   face thickness Hf = (Ha + Hb)/2, limited to |q| <= H_donor * dn / (4 dt).
+// Rows outside the shard come from the halo [2][nx] (s, H) when present,
+// otherwise the edge row is replicated (domain edge: no face, zero flux).
+struct FlowGrid {
+  const void* elev;            // R[n_pad]
+  const double* iwe;           // st + S_HIWE * n_pad
+  const double* hn;            // north halo [2][nx] or null
+  const double* hs;            // south halo [2][nx] or null
+  int64_t ny, nx;
+  double wi;
+};
+template <class R>
+__device__ __forceinline__ double flow_H(const FlowGrid& g, int64_t r, int64_t c) {
+  if (r < 0) return g.hn[g.nx + c];
+  if (r >= g.ny) return g.hs[g.nx + c];
+  return g.iwe[r * g.nx + c] * g.wi;
+}
+template <class R>
+__device__ __forceinline__ double flow_S(const FlowGrid& g, int64_t r, int64_t c) {
+#pragma clang fp contract(off)
+  c = c < 0 ? 0 : (c >= g.nx ? g.nx - 1 : c);
+  if (r < 0) { if (g.hn) return g.hn[c]; r = 0; }
+  if (r >= g.ny) { if (g.hs) return g.hs[c]; r = g.ny - 1; }
+  const int64_t i = r * g.nx + c;
+  return (double)static_cast<const R*>(g.elev)[i] + g.iwe[i] * g.wi;
+}
+__device__ __forceinline__ double flow_face_D(double Ha, double Hb, double gn, double gt, double gamma) {
+#pragma clang fp contract(off)
+  const double Hf = 0.5 * (Ha + Hb);
+  const double h2 = Hf * Hf;
+  const double h5 = (h2 * h2) * Hf;
+  return (gamma * h5) * (gn * gn + gt * gt);
+}
+__device__ __forceinline__ double flow_face_q(double Ha, double Hb, double gn, double gt, double gamma, double dn,
+                                              double dt) {
+#pragma clang fp contract(off)
+  double q = -(flow_face_D(Ha, Hb, gn, gt, gamma) * gn);
+  const double Hd = q > 0.0 ? Ha : Hb;
+  const double qlim = (Hd * dn) / (4.0 * dt);
+  return fmin(fmax(q, -qlim), qlim);
+}
+// face between (r, c) and (r, c+1): returns (gn, gt) through refs
+template <class R>
+__device__ __forceinline__ void flow_grad_x(const FlowGrid& g, int64_t r, int64_t c, double dx, double dy, double& gn,
+                                            double& gt) {
+#pragma clang fp contract(off)
+  gn = (flow_S<R>(g, r, c + 1) - flow_S<R>(g, r, c)) / dx;
+  gt = ((flow_S<R>(g, r + 1, c) - flow_S<R>(g, r - 1, c)) + (flow_S<R>(g, r + 1, c + 1) - flow_S<R>(g, r - 1, c + 1))) /
+       (4.0 * dy);
+}
+// face between (r, c) and (r+1, c)
+template <class R>
+__device__ __forceinline__ void flow_grad_y(const FlowGrid& g, int64_t r, int64_t c, double dx, double dy, double& gn,
+                                            double& gt) {
+#pragma clang fp contract(off)
+  gn = (flow_S<R>(g, r + 1, c) - flow_S<R>(g, r, c)) / dy;
+  gt = ((flow_S<R>(g, r, c + 1) - flow_S<R>(g, r, c - 1)) + (flow_S<R>(g, r + 1, c + 1) - flow_S<R>(g, r + 1, c - 1))) /
+       (4.0 * dx);
+}
+
+template <class R>
+__global__ void k_ice_flow(const FlowGrid g, double dx, double dy, double dt, double gamma, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int64_t n = g.ny * g.nx;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / g.nx, c = i % g.nx;
+    double gn, gt, qE = 0.0, qW = 0.0, qS = 0.0, qN = 0.0;
+    if (c + 1 < g.nx) {
+      flow_grad_x<R>(g, r, c, dx, dy, gn, gt);
+      qE = flow_face_q(flow_H<R>(g, r, c), flow_H<R>(g, r, c + 1), gn, gt, gamma, dx, dt);
+    }
+    if (c > 0) {
+      flow_grad_x<R>(g, r, c - 1, dx, dy, gn, gt);
+      qW = flow_face_q(flow_H<R>(g, r, c - 1), flow_H<R>(g, r, c), gn, gt, gamma, dx, dt);
+    }
+    if (r + 1 < g.ny || g.hs) {
+      flow_grad_y<R>(g, r, c, dx, dy, gn, gt);
+      qS = flow_face_q(flow_H<R>(g, r, c), flow_H<R>(g, r + 1, c), gn, gt, gamma, dy, dt);
+    }
+    if (r > 0 || g.hn) {
+      flow_grad_y<R>(g, r - 1, c, dx, dy, gn, gt);
+      qN = flow_face_q(flow_H<R>(g, r - 1, c), flow_H<R>(g, r, c), gn, gt, gamma, dy, dt);
+    }
+    const double div = (qE - qW) / dx + (qS - qN) / dy;
+    out[i] = fmax(g.iwe[i] - (dt / g.wi) * div, 0.0);
+  }
+}
+
+// per-block max of the face diffusivity over the east and south faces of
+// every cell, plus the north face of row 0 when a north halo is present
+template <class R>
+__global__ __launch_bounds__(256) void k_ice_flow_dmax(const FlowGrid g, double dx, double dy, double gamma,
+                                                       double* __restrict__ bmax) {
+  __shared__ double red[256];
+  const int64_t n = g.ny * g.nx;
+  double m = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / g.nx, c = i % g.nx;
+    double gn, gt;
+    if (c + 1 < g.nx) {
+      flow_grad_x<R>(g, r, c, dx, dy, gn, gt);
+      m = fmax(m, flow_face_D(flow_H<R>(g, r, c), flow_H<R>(g, r, c + 1), gn, gt, gamma));
+    }
+    if (r + 1 < g.ny || g.hs) {
+      flow_grad_y<R>(g, r, c, dx, dy, gn, gt);
+      m = fmax(m, flow_face_D(flow_H<R>(g, r, c), flow_H<R>(g, r + 1, c), gn, gt, gamma));
+    }
+    if (r == 0 && g.hn) {
+      flow_grad_y<R>(g, -1, c, dx, dy, gn, gt);
+      m = fmax(m, flow_face_D(flow_H<R>(g, -1, c), flow_H<R>(g, 0, c), gn, gt, gamma));
+    }
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) bmax[blockIdx.x] = red[0];
+}
+
+__global__ void k_flow_ice_depth(double* __restrict__ st, int64_t n, int64_t n_pad, double wi) {
+#pragma clang fp contract(off)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    st[S_HICE * n_pad + i] = st[S_HIWE * n_pad + i] * wi;
+}
+
+// this shard's first / last rows as halo rows [2][nx] (s, H) for its neighbours
+template <class R>
+__global__ void k_ice_flow_edges(const FlowGrid g, double* __restrict__ first, double* __restrict__ last) {
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < g.nx; c += (int64_t)gridDim.x * blockDim.x) {
+    first[c] = flow_S<R>(g, 0, c);
+    first[g.nx + c] = flow_H<R>(g, 0, c);
+    last[c] = flow_S<R>(g, g.ny - 1, c);
+    last[g.nx + c] = flow_H<R>(g, g.ny - 1, c);
+  }
+}
+
 // tfg_set_inputs / tfg_get_outputs: the per-step BMI traffic of one call each.
 // src [5][n]: P_air, Hum_sp, P, T_air, uz (BMI order) -> frame planes.
 template <class R, class S>
@@ -738,6 +886,10 @@ struct tfg_handle {
   bool tot_dirty = false;        // window slots set through TFG_ST_WINDOW
   double* wtmp = nullptr;        // [n_pad] f64 scratch for window I/O
   double* halo = nullptr;        // [2][nx] f64 DEM halo rows (tfg_terrain_from_dem)
+  double* flow_halo = nullptr;   // [2 sides][2][nx] f64 ice-flow halo rows (s, H)
+  double* flow_edges = nullptr;  // [2 rows][2][nx] f64 this shard's edge rows
+  double* flow_red = nullptr;    // [8192] f64 per-block maxima
+  double flow_gamma = 0.0;       // 2A/(n+2) (rho_ice g)^n, n = 3 [m^-3 yr^-1]
   // tfg_set_inputs: pinned host staging ring (2 slots) + device staging
   void* in_h[2] = {nullptr, nullptr};
   void* in_d[2] = {nullptr, nullptr};
@@ -997,7 +1149,7 @@ extern "C" {
 int tfg_abi_version(void) { return TFG_ABI_VERSION; }
 
 const char* tfg_build_info(void) {
-  return "libtfg abi=2 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
+  return "libtfg abi=3 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
          "k_diag_reduce, k_fill_synthetic";
 }
 
@@ -1044,6 +1196,10 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->n_catch = n_catch;
   h->ring_len = p->ring_len;
   derive_params(*p, h->dp);
+  {
+    const double rg = p->rho_ice * p->g;  // Glen's law n = 3: Gamma = 2A/5 (rho_ice g)^3
+    h->flow_gamma = 2.0 * p->glens_A / 5.0 * (rg * rg * rg);
+  }
   if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TFG_ERR_HIP); }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { h->err = "hipGetDeviceProperties failed"; return bail(TFG_ERR_HIP); }
@@ -1097,6 +1253,7 @@ int tfg_destroy(tfg_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
+                  h->flow_halo, h->flow_edges, h->flow_red,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
@@ -1607,6 +1764,92 @@ int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_n
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->geo_dirty = true;
   h->slope_invalid = false;  // tan(beta) >= 0 always maps into [0, pi/2)
+  return TFG_OK;
+}
+
+
+namespace {
+// Ice-flow halos into h->flow_halo; FlowGrid over this shard.
+int flow_setup(tfg_handle* h, const double* hn, const double* hs, int on_dev, FlowGrid& g) {
+  if (!h->initialised) return fail(h, TFG_ERR_STATE, "tfg_init_state() has not been called");
+  const int64_t nx = h->nx;
+  if (!h->flow_halo) HIPCHK(h, hipMalloc((void**)&h->flow_halo, (size_t)4 * nx * 8));
+  if (hn) HIPCHK(h, hipMemcpyAsync(h->flow_halo, hn, (size_t)2 * nx * 8, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+  if (hs) HIPCHK(h, hipMemcpyAsync(h->flow_halo + 2 * nx, hs, (size_t)2 * nx * 8, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+  g.elev = h->stat;
+  g.iwe = h->st + S_HIWE * h->n_pad;
+  g.hn = hn ? h->flow_halo : nullptr;
+  g.hs = hs ? h->flow_halo + 2 * nx : nullptr;
+  g.ny = h->ny;
+  g.nx = nx;
+  g.wi = h->dp.wi;
+  return TFG_OK;
+}
+}  // namespace
+
+int tfg_ice_flow_edges(tfg_handle* h, double* first, double* last, int on_device) {
+  if (!h || !first || !last) return fail(h, TFG_ERR_ARG, "null argument");
+  HIPCHK(h, hipSetDevice(h->device));
+  FlowGrid g;
+  if (int rc = flow_setup(h, nullptr, nullptr, 0, g)) return rc;
+  const int64_t nx = h->nx;
+  if (!h->flow_edges) HIPCHK(h, hipMalloc((void**)&h->flow_edges, (size_t)4 * nx * 8));
+  const int gb = grid_for(nx);
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_ice_flow_edges<float>), gb, 256, 0, h->stream, g, h->flow_edges, h->flow_edges + 2 * nx);
+  else
+    hipLaunchKernelGGL((k_ice_flow_edges<double>), gb, 256, 0, h->stream, g, h->flow_edges, h->flow_edges + 2 * nx);
+  HIPCHK(h, hipGetLastError());
+  const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  HIPCHK(h, hipMemcpyAsync(first, h->flow_edges, (size_t)2 * nx * 8, k, h->stream));
+  HIPCHK(h, hipMemcpyAsync(last, h->flow_edges + 2 * nx, (size_t)2 * nx * 8, k, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_north, const double* halo_south,
+                      int halo_on_device, double* dmax) {
+  if (!h || !dmax) return fail(h, TFG_ERR_ARG, "null argument");
+  if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
+  HIPCHK(h, hipSetDevice(h->device));
+  FlowGrid g;
+  if (int rc = flow_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
+  const int gb = grid_for(h->n);
+  if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)8192 * 8));
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_ice_flow_dmax<float>), gb, 256, 0, h->stream, g, dx, dy, h->flow_gamma, h->flow_red);
+  else
+    hipLaunchKernelGGL((k_ice_flow_dmax<double>), gb, 256, 0, h->stream, g, dx, dy, h->flow_gamma, h->flow_red);
+  HIPCHK(h, hipGetLastError());
+  std::vector<double> bm(gb);
+  HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  double m = 0.0;
+  for (double v : bm) m = std::max(m, v);
+  *dmax = m;
+  return TFG_OK;
+}
+
+int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
+                      const double* halo_south, int halo_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!(dx > 0) || !(dy > 0) || !(dt_years > 0)) return fail(h, TFG_ERR_ARG, "dt, dx and dy must be > 0");
+  HIPCHK(h, hipSetDevice(h->device));
+  FlowGrid g;
+  if (int rc = flow_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
+  if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
+  const int gb = grid_for(h->n);
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((k_ice_flow<float>), gb, 256, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+  else
+    hipLaunchKernelGGL((k_ice_flow<double>), gb, 256, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+  HIPCHK(h, hipGetLastError());
+  double* iwe = h->st + S_HIWE * h->n_pad;
+  HIPCHK(h, hipMemcpyAsync(iwe, h->wtmp, (size_t)h->n * 8, hipMemcpyDeviceToDevice, h->stream));
+  // the next step's previous-step ice depth (:1726) when it is read from the state plane
+  hipLaunchKernelGGL(k_flow_ice_depth, grid_for(h->n), 256, 0, h->stream, h->st, h->n, h->n_pad, h->dp.wi);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;
 }
 

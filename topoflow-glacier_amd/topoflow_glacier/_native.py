@@ -20,6 +20,7 @@ __all__ = [
 
 LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
 
+ABI_VERSION = 3  # include/tfg.h TFG_ABI_VERSION
 F32, F64, I32 = 0, 1, 2
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_DOMAIN = 0, 1, 2, 3, 4
 
@@ -48,7 +49,7 @@ class TfgParams(ctypes.Structure):
         "rho_air", "rho_snow", "rho_ice", "rho_H2O", "h_active_layer", "T0",
         "Cp_air", "Cp_ice", "Cp_snow", "g", "Lf", "eps", "kappa", "latent_heat_constant", "Lv",
         "sigma", "sea_level_p0", "uni_gas_const", "M_mass_air", "z0_air", "em_surf",
-    )] + [("satterlund", ctypes.c_int32), ("ring_len", ctypes.c_int32)]
+    )] + [("satterlund", ctypes.c_int32), ("ring_len", ctypes.c_int32), ("glens_A", ctypes.c_double)]
 
 
 # tfg_uniforms, one record per time step (numpy structured dtype, C layout)
@@ -107,6 +108,9 @@ def load() -> ctypes.CDLL:
         "tfg_fill_synthetic": ([vp, ctypes.c_uint64, i64, i64, ctypes.POINTER(ctypes.c_float), i32], i32),
         "tfg_last_error": ([vp], ctypes.c_char_p),
         "tfg_terrain_from_dem": ([vp, ctypes.c_double, ctypes.c_double, vp, vp, i32, i32], i32),
+        "tfg_ice_flow_edges": ([vp, dp, dp, i32], i32),
+        "tfg_ice_flow_dmax": ([vp, ctypes.c_double, ctypes.c_double, dp, dp, i32, dp], i32),
+        "tfg_ice_flow_step": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32], i32),
         "tfg_set_inputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),
@@ -115,8 +119,8 @@ def load() -> ctypes.CDLL:
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    if L.tfg_abi_version() != 2:
-        raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != 2 (rebuild the library)")
+    if L.tfg_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != {ABI_VERSION} (rebuild the library)")
     _lib = L
     return L
 
@@ -138,6 +142,6 @@ def exported_symbols() -> list[str]:
         "tfg_abi_version", "tfg_build_info", "tfg_device_count", "tfg_create", "tfg_destroy",
         "tfg_set_stream", "tfg_get_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
-        "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_set_inputs", "tfg_get_outputs",
+        "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update",
     ) if hasattr(L, n)]

@@ -278,6 +278,43 @@ class GlacierEngine:
             torch.cuda.current_stream(keep[0].device).synchronize()
         self._chk(self.lib.tfg_terrain_from_dem(self.h, float(dx), float(dy), ptrs[0], ptrs[1], dtype, on_dev))
 
+    # -- optional lateral ice flow (tfg_ice_flow_*, off unless called) -----------------
+    @staticmethod
+    def _halo_ptr(halo, nx):
+        if halo is None:
+            return None, None
+        a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(2, nx))
+        return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+    def ice_flow_edges(self) -> tuple[np.ndarray, np.ndarray]:
+        """This shard's first and last rows as ice-flow halo rows, [2][nx] each
+        (surface elevation, ice thickness)."""
+        first, last = np.empty((2, self.nx)), np.empty((2, self.nx))
+        dp = ctypes.POINTER(ctypes.c_double)
+        self._chk(self.lib.tfg_ice_flow_edges(self.h, first.ctypes.data_as(dp), last.ctypes.data_as(dp), 0))
+        return first, last
+
+    def ice_flow_dmax(self, dx: float, dy: float, north=None, south=None) -> float:
+        """Largest face diffusivity [m2 yr-1] (sets the stable sub-step)."""
+        kn, pn = self._halo_ptr(north, self.nx)
+        ks, ps = self._halo_ptr(south, self.nx)
+        out = ctypes.c_double()
+        self._chk(self.lib.tfg_ice_flow_dmax(self.h, float(dx), float(dy), pn, ps, 0, ctypes.byref(out)))
+        return out.value
+
+    def ice_flow_step(self, dt_years: float, dx: float, dy: float, north=None, south=None) -> None:
+        """One explicit shallow-ice sub-step of dt_years (tfg_ice_flow_step)."""
+        kn, pn = self._halo_ptr(north, self.nx)
+        ks, ps = self._halo_ptr(south, self.nx)
+        self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, 0))
+
+    def ice_flow(self, dt_years: float, dx: float, dy: float, cfl: float = 0.5) -> int:
+        """Move ice for dt_years on this shard alone (domain edges all round),
+        in as many stable sub-steps as needed; returns the sub-step count."""
+        from topoflow_glacier.sharding import ice_flow
+
+        return ice_flow(self, dt_years, dx, dy, cfl=cfl, distributed=False)
+
     # -- mass balance -------------------------------------------------------------
     def diagnostics(self) -> np.ndarray:
         """[n_catch][6] = vol_P, vol_PR, vol_PS, vol_SM, vol_IM, P_max of this shard."""
