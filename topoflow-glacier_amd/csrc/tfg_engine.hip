@@ -788,10 +788,16 @@ __global__ __launch_bounds__(256) void k_ice_flow_dmax(const FlowGrid g, double 
   if (threadIdx.x == 0) bmax[blockIdx.x] = red[0];
 }
 
-__global__ void k_flow_ice_depth(double* __restrict__ st, int64_t n, int64_t n_pad, double wi) {
+// commit a sub-step: the new h_iwe into the state plane, and the next step's
+// previous-step ice depth h_ice = h_iwe * wi (:1726) for the state-plane read
+__global__ void k_flow_commit(double* __restrict__ st, const double* __restrict__ iwe_new, int64_t n, int64_t n_pad,
+                              double wi) {
 #pragma clang fp contract(off)
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    st[S_HICE * n_pad + i] = st[S_HIWE * n_pad + i] * wi;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = iwe_new[i];
+    st[S_HIWE * n_pad + i] = v;
+    st[S_HICE * n_pad + i] = v * wi;
+  }
 }
 
 // this shard's first / last rows as halo rows [2][nx] (s, H) for its neighbours
@@ -1844,10 +1850,7 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   else
     hipLaunchKernelGGL((k_ice_flow<double>), gb, 256, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
   HIPCHK(h, hipGetLastError());
-  double* iwe = h->st + S_HIWE * h->n_pad;
-  HIPCHK(h, hipMemcpyAsync(iwe, h->wtmp, (size_t)h->n * 8, hipMemcpyDeviceToDevice, h->stream));
-  // the next step's previous-step ice depth (:1726) when it is read from the state plane
-  hipLaunchKernelGGL(k_flow_ice_depth, grid_for(h->n), 256, 0, h->stream, h->st, h->n, h->n_pad, h->dp.wi);
+  hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;

@@ -214,6 +214,7 @@ class BmiTopoflowGlacier(BmiBase):
         self._stale.clear()
         self._dirty_outputs: set[str] = set()
         self._timestep = 0
+        self._flowed_at = 0
         start = parse_time(cfg.start_time)
         self.start_year, self.start_month, self.start_day, self.start_hour = start.year, start.month, start.day, start.hour
         end = parse_time(cfg.end_time)
@@ -266,6 +267,17 @@ class BmiTopoflowGlacier(BmiBase):
     GMT_offset = property(lambda self: self._calendar()[4])
     TSN_offset = property(lambda self: self._calendar()[5])
 
+    def _flow_if_due(self) -> None:
+        """The optional ice-flow term (config ``ice_flow``): between step
+        k*ice_flow_interval and the next one, move ice for that interval
+        (dt hours / 8760 per year).  Off by default (the reference moves no ice)."""
+        c = self.cfg
+        if c.ice_flow and self._timestep > 0 and self._timestep % c.ice_flow_interval == 0 \
+                and self._flowed_at != self._timestep:
+            self._engine.ice_flow(c.ice_flow_interval * c.dt / 8760.0, c.dx, c.dy)
+            self._flowed_at = self._timestep
+            self._stale = {_int(n) for n, _ in _output_vars}
+
     def update(self) -> None:
         """Advance one time step (reference :413-465) on the GPU.  Small
         models (eager mirrors) take one synchronous tfg_update call: inputs in,
@@ -273,11 +285,13 @@ class BmiTopoflowGlacier(BmiBase):
         eng = self._require()
         if not self._eager:
             self._push_inputs()
+            self._flow_if_due()
             eng.run(1)
             self._after_steps(1)
             return
         if self._dirty_outputs:
             self._push_dirty_outputs()
+        self._flow_if_due()
         block = self._in_block
         for i, v in enumerate(self._in_mirrors):
             block[i] = v
@@ -300,8 +314,15 @@ class BmiTopoflowGlacier(BmiBase):
             return None
         eng = self._require()
         self._push_inputs()
-        eng.run(n_steps)
-        self._after_steps(n_steps)
+        done = 0
+        while done < n_steps:  # in chunks that end where the ice-flow term is due
+            self._flow_if_due()
+            k = n_steps - done
+            if self.cfg.ice_flow:
+                k = min(k, self.cfg.ice_flow_interval - self._timestep % self.cfg.ice_flow_interval)
+            eng.run(k)
+            self._after_steps(k)
+            done += k
 
     def finalize(self) -> None:
         """Release the device shard (reference :467-469)."""

@@ -15,7 +15,10 @@ deliberate, additive differences:
   catchment), ``engine`` ("float64" | "float32"; default float64 for one cell,
   float32 for grids), ``device`` (HIP device ordinal, default LOCAL_RANK or 0),
   ``time_zone`` (IANA name; default looked up from lat/lon),
-  ``fuse_steps`` (time steps fused per kernel launch, default 24).
+  ``fuse_steps`` (time steps fused per kernel launch, default 24),
+  ``ice_flow`` / ``ice_flow_interval`` / ``dx`` / ``dy`` (the optional
+  shallow-ice flow term, off by default; it moves ice between cells every
+  ``ice_flow_interval`` steps on a grid of dx x dy metre cells).
 
 Unknown keys are ignored, as in the reference (pydantic default).
 """
@@ -24,7 +27,7 @@ from __future__ import annotations
 
 from typing import Literal
 
-from pydantic import BaseModel, ConfigDict, Field, field_validator
+from pydantic import BaseModel, ConfigDict, Field, field_validator, model_validator
 
 __all__ = ["TopoflowGlacierConfig"]
 
@@ -109,6 +112,18 @@ class TopoflowGlacierConfig(BaseModel):
     device: int | None = None
     time_zone: str | None = None
     fuse_steps: int = Field(24, ge=1)
+    # optional lateral ice flow (extension; tfg_ice_flow_*): off by default,
+    # which keeps results identical to the reference
+    ice_flow: bool = False
+    ice_flow_interval: int = Field(24, ge=1)  # time steps between flow updates
+    dx: float | None = Field(None, gt=0)      # grid spacing [m], west-east
+    dy: float | None = Field(None, gt=0)      # grid spacing [m], north-south
+
+    @model_validator(mode="after")
+    def _flow_needs_spacing(self):
+        if self.ice_flow and (self.dx is None or self.dy is None):
+            raise ValueError("ice_flow needs the grid spacing dx and dy [m]")
+        return self
 
     @field_validator("start_time", "end_time", mode="before")
     @classmethod
