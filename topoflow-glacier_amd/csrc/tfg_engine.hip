@@ -708,84 +708,86 @@ __device__ __forceinline__ double flow_face_q(double Ha, double Hb, double gn, d
   const double qlim = (Hd * dn) / (4.0 * dt);
   return fmin(fmax(q, -qlim), qlim);
 }
-// face between (r, c) and (r, c+1): returns (gn, gt) through refs
-template <class R>
-__device__ __forceinline__ void flow_grad_x(const FlowGrid& g, int64_t r, int64_t c, double dx, double dy, double& gn,
-                                            double& gt) {
+// One sub-step, LDS-tiled: a workgroup owns kFlowTX columns x kFlowRows rows
+// and walks down its strip with a three-row ring of (s, H) in LDS (one halo
+// column each side).  Each face flux is evaluated once per workgroup: the
+// row's x-faces into LDS, the y-face below each cell in a register that
+// becomes the next row's north face.  A face shared by two workgroups (or two
+// shards) is computed by both from the same values in the same order, so they
+// agree bit for bit (restatement: tests/harness.py:ice_flow_step_restated).
+// DMAX: instead of stepping, the largest face diffusivity of the workgroup's
+// faces goes to out[workgroup] (the CFL bound of tfg_ice_flow_dmax).
+constexpr int kFlowTX = 256, kFlowRows = 32;
+template <class R, bool DMAX>
+__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, double dx, double dy, double dt, double gamma,
+                                                      double* __restrict__ out) {
 #pragma clang fp contract(off)
-  gn = (flow_S<R>(g, r, c + 1) - flow_S<R>(g, r, c)) / dx;
-  gt = ((flow_S<R>(g, r + 1, c) - flow_S<R>(g, r - 1, c)) + (flow_S<R>(g, r + 1, c + 1) - flow_S<R>(g, r - 1, c + 1))) /
-       (4.0 * dy);
-}
-// face between (r, c) and (r+1, c)
-template <class R>
-__device__ __forceinline__ void flow_grad_y(const FlowGrid& g, int64_t r, int64_t c, double dx, double dy, double& gn,
-                                            double& gt) {
-#pragma clang fp contract(off)
-  gn = (flow_S<R>(g, r + 1, c) - flow_S<R>(g, r, c)) / dy;
-  gt = ((flow_S<R>(g, r, c + 1) - flow_S<R>(g, r, c - 1)) + (flow_S<R>(g, r + 1, c + 1) - flow_S<R>(g, r + 1, c - 1))) /
-       (4.0 * dx);
-}
-
-template <class R>
-__global__ void k_ice_flow(const FlowGrid g, double dx, double dy, double dt, double gamma, double* __restrict__ out) {
-#pragma clang fp contract(off)
-  const int64_t n = g.ny * g.nx;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / g.nx, c = i % g.nx;
-    double gn, gt, qE = 0.0, qW = 0.0, qS = 0.0, qN = 0.0;
-    if (c + 1 < g.nx) {
-      flow_grad_x<R>(g, r, c, dx, dy, gn, gt);
-      qE = flow_face_q(flow_H<R>(g, r, c), flow_H<R>(g, r, c + 1), gn, gt, gamma, dx, dt);
+  __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], qx[kFlowTX + 1];
+  double dmax = 0.0;
+  const int t = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * kFlowTX;
+  const int64_t r0 = (int64_t)blockIdx.y * kFlowRows;
+  const int64_t r1 = r0 + kFlowRows < g.ny ? r0 + kFlowRows : g.ny;
+  const int64_t c = c0 + t;
+  auto slot = [&](int64_t rr) { return (int)((rr - r0 + 1) % 3); };
+  auto load = [&](int64_t rr) {
+    const int sl = slot(rr);
+    const bool no_row = (rr < 0 && !g.hn) || (rr >= g.ny && !g.hs);
+    for (int k = t; k < kFlowTX + 2; k += kFlowTX) {
+      const int64_t cc = c0 - 1 + k;
+      sS[sl][k] = flow_S<R>(g, rr, cc);
+      const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
+      sH[sl][k] = no_row ? 0.0 : flow_H<R>(g, rr, cl);
     }
-    if (c > 0) {
-      flow_grad_x<R>(g, r, c - 1, dx, dy, gn, gt);
-      qW = flow_face_q(flow_H<R>(g, r, c - 1), flow_H<R>(g, r, c), gn, gt, gamma, dx, dt);
+  };
+  auto face_y = [&](int a, int b) {  // between the rows in slots a (north) and b (south), column c
+    const double gn = (sS[b][t + 1] - sS[a][t + 1]) / dy;
+    const double gt = ((sS[a][t + 2] - sS[a][t]) + (sS[b][t + 2] - sS[b][t])) / (4.0 * dx);
+    if constexpr (DMAX) {
+      if (c < g.nx) dmax = fmax(dmax, flow_face_D(sH[a][t + 1], sH[b][t + 1], gn, gt, gamma));
+      return 0.0;
     }
-    if (r + 1 < g.ny || g.hs) {
-      flow_grad_y<R>(g, r, c, dx, dy, gn, gt);
-      qS = flow_face_q(flow_H<R>(g, r, c), flow_H<R>(g, r + 1, c), gn, gt, gamma, dy, dt);
-    }
-    if (r > 0 || g.hn) {
-      flow_grad_y<R>(g, r - 1, c, dx, dy, gn, gt);
-      qN = flow_face_q(flow_H<R>(g, r - 1, c), flow_H<R>(g, r, c), gn, gt, gamma, dy, dt);
-    }
-    const double div = (qE - qW) / dx + (qS - qN) / dy;
-    out[i] = fmax(g.iwe[i] - (dt / g.wi) * div, 0.0);
-  }
-}
-
-// per-block max of the face diffusivity over the east and south faces of
-// every cell, plus the north face of row 0 when a north halo is present
-template <class R>
-__global__ __launch_bounds__(256) void k_ice_flow_dmax(const FlowGrid g, double dx, double dy, double gamma,
-                                                       double* __restrict__ bmax) {
-  __shared__ double red[256];
-  const int64_t n = g.ny * g.nx;
-  double m = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = i / g.nx, c = i % g.nx;
-    double gn, gt;
-    if (c + 1 < g.nx) {
-      flow_grad_x<R>(g, r, c, dx, dy, gn, gt);
-      m = fmax(m, flow_face_D(flow_H<R>(g, r, c), flow_H<R>(g, r, c + 1), gn, gt, gamma));
-    }
-    if (r + 1 < g.ny || g.hs) {
-      flow_grad_y<R>(g, r, c, dx, dy, gn, gt);
-      m = fmax(m, flow_face_D(flow_H<R>(g, r, c), flow_H<R>(g, r + 1, c), gn, gt, gamma));
-    }
-    if (r == 0 && g.hn) {
-      flow_grad_y<R>(g, -1, c, dx, dy, gn, gt);
-      m = fmax(m, flow_face_D(flow_H<R>(g, -1, c), flow_H<R>(g, 0, c), gn, gt, gamma));
-    }
-  }
-  red[threadIdx.x] = m;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    return flow_face_q(sH[a][t + 1], sH[b][t + 1], gn, gt, gamma, dy, dt);
+  };
+  load(r0 - 1);
+  load(r0);
+  double qN = 0.0;
+  for (int64_t r = r0; r < r1; ++r) {
+    __syncthreads();  // row r-2's slot and qx are free
+    load(r + 1);
     __syncthreads();
+    const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
+    for (int k = t; k < kFlowTX + 1; k += kFlowTX) {  // x-faces between columns c0-1+k and c0+k
+      const int64_t fc = c0 - 1 + k;
+      double q = 0.0;
+      if (fc >= 0 && fc + 1 < g.nx) {
+        const double gn = (sS[rc][k + 1] - sS[rc][k]) / dx;
+        const double gt = ((sS[rp][k] - sS[rm][k]) + (sS[rp][k + 1] - sS[rm][k + 1])) / (4.0 * dy);
+        if constexpr (DMAX) dmax = fmax(dmax, flow_face_D(sH[rc][k], sH[rc][k + 1], gn, gt, gamma));
+        else q = flow_face_q(sH[rc][k], sH[rc][k + 1], gn, gt, gamma, dx, dt);
+      }
+      qx[k] = q;
+    }
+    if (r == r0) qN = (r > 0 || g.hn) ? face_y(rm, rc) : 0.0;
+    const double qS = (r + 1 < g.ny || g.hs) ? face_y(rc, rp) : 0.0;
+    __syncthreads();  // qx complete
+    if (!DMAX && c < g.nx) {
+      const int64_t i = r * g.nx + c;
+      const double div = (qx[t + 1] - qx[t]) / dx + (qS - qN) / dy;
+      out[i] = fmax(g.iwe[i] - (dt / g.wi) * div, 0.0);
+    }
+    qN = qS;
   }
-  if (threadIdx.x == 0) bmax[blockIdx.x] = red[0];
+  if constexpr (DMAX) {
+    __syncthreads();
+    qx[t] = dmax;  // reuse qx as the reduction buffer
+    __syncthreads();
+    for (int w = kFlowTX / 2; w > 0; w >>= 1) {
+      if (t < w) qx[t] = fmax(qx[t], qx[t + w]);
+      __syncthreads();
+    }
+    if (t == 0) out[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = qx[0];
+  }
 }
 
 // commit a sub-step: the new h_iwe into the state plane, and the next step's
@@ -894,7 +896,7 @@ struct tfg_handle {
   double* halo = nullptr;        // [2][nx] f64 DEM halo rows (tfg_terrain_from_dem)
   double* flow_halo = nullptr;   // [2 sides][2][nx] f64 ice-flow halo rows (s, H)
   double* flow_edges = nullptr;  // [2 rows][2][nx] f64 this shard's edge rows
-  double* flow_red = nullptr;    // [8192] f64 per-block maxima
+  double* flow_red = nullptr;    // f64 per-workgroup maxima of k_ice_flow<R, true>
   double flow_gamma = 0.0;       // 2A/(n+2) (rho_ice g)^n, n = 3 [m^-3 yr^-1]
   // tfg_set_inputs: pinned host staging ring (2 slots) + device staging
   void* in_h[2] = {nullptr, nullptr};
@@ -1820,12 +1822,14 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
   HIPCHK(h, hipSetDevice(h->device));
   FlowGrid g;
   if (int rc = flow_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
-  const int gb = grid_for(h->n);
-  if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)8192 * 8));
+  const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
+  if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
+  const int64_t gb = (int64_t)fgrid.x * fgrid.y;
+  if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)gb * 8));  // the grid never changes
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow_dmax<float>), gb, 256, 0, h->stream, g, dx, dy, h->flow_gamma, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, 1.0, h->flow_gamma, h->flow_red);
   else
-    hipLaunchKernelGGL((k_ice_flow_dmax<double>), gb, 256, 0, h->stream, g, dx, dy, h->flow_gamma, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, 1.0, h->flow_gamma, h->flow_red);
   HIPCHK(h, hipGetLastError());
   std::vector<double> bm(gb);
   HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1844,11 +1848,12 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   FlowGrid g;
   if (int rc = flow_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
   if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
-  const int gb = grid_for(h->n);
+  const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
+  if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float>), gb, 256, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+    hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
   else
-    hipLaunchKernelGGL((k_ice_flow<double>), gb, 256, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+    hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
   HIPCHK(h, hipGetLastError());
   hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
