@@ -328,10 +328,10 @@ def _flow_faces(elev, iwe, wi, gamma, dx, dy, north, south):
     P = np.vstack([Sn[None], S, Ss[None]])
     P = np.hstack([P[:, :1], P, P[:, -1:]])  # rows -1..ny, columns -1..nx (edge replicated)
     Hp = np.vstack([Hn[None], H, Hs[None]])
-    gnx = (P[1:-1, 2:-1] - P[1:-1, 1:-2]) / dx
-    gtx = ((P[2:, 1:-2] - P[:-2, 1:-2]) + (P[2:, 2:-1] - P[:-2, 2:-1])) / (4.0 * dy)
-    gny = (P[1:, 1:-1] - P[:-1, 1:-1]) / dy
-    gty = ((P[:-1, 2:] - P[:-1, :-2]) + (P[1:, 2:] - P[1:, :-2])) / (4.0 * dx)
+    gnx = (P[1:-1, 2:-1] - P[1:-1, 1:-2]) * (1.0 / dx)
+    gtx = ((P[2:, 1:-2] - P[:-2, 1:-2]) + (P[2:, 2:-1] - P[:-2, 2:-1])) * (1.0 / (4.0 * dy))
+    gny = (P[1:, 1:-1] - P[:-1, 1:-1]) * (1.0 / dy)
+    gty = ((P[:-1, 2:] - P[:-1, :-2]) + (P[1:, 2:] - P[1:, :-2])) * (1.0 / (4.0 * dx))
     return H, Hp, gnx, gtx, gny, gty
 
 
@@ -345,7 +345,7 @@ def _face_D(Ha, Hb, gn, gt, gamma):
 def _face_q(Ha, Hb, gn, gt, gamma, dn, dt):
     q = -(_face_D(Ha, Hb, gn, gt, gamma) * gn)
     Hd = np.where(q > 0.0, Ha, Hb)
-    qlim = (Hd * dn) / (4.0 * dt)
+    qlim = Hd * (dn / (4.0 * dt))
     return np.minimum(np.maximum(q, -qlim), qlim)
 
 
@@ -363,7 +363,7 @@ def ice_flow_step_restated(elev, iwe, wi, gamma, dx, dy, dt, north=None, south=N
     z = np.zeros((ny, 1))
     qE = np.hstack([qx, z])
     qW = np.hstack([z, qx])
-    div = (qE - qW) / dx + (qy[1:] - qy[:-1]) / dy
+    div = (qE - qW) * (1.0 / dx) + (qy[1:] - qy[:-1]) * (1.0 / dy)
     return np.maximum(np.asarray(iwe, np.float64) - (dt / wi) * div, 0.0)
 
 

@@ -700,13 +700,24 @@ __device__ __forceinline__ double flow_face_D(double Ha, double Hb, double gn, d
   const double h5 = (h2 * h2) * Hf;
   return (gamma * h5) * (gn * gn + gt * gt);
 }
-__device__ __forceinline__ double flow_face_q(double Ha, double Hb, double gn, double gt, double gamma, double dn,
-                                              double dt) {
+// lim = dn / (4 dt): a face passes at most a quarter of the donor's ice
+__device__ __forceinline__ double flow_face_q(double Ha, double Hb, double gn, double gt, double gamma, double lim) {
 #pragma clang fp contract(off)
   double q = -(flow_face_D(Ha, Hb, gn, gt, gamma) * gn);
   const double Hd = q > 0.0 ? Ha : Hb;
-  const double qlim = (Hd * dn) / (4.0 * dt);
+  const double qlim = Hd * lim;
   return fmin(fmax(q, -qlim), qlim);
+}
+// Per-launch constants of a sub-step: the kernel multiplies, it never divides
+// (fp64 division would make the stencil issue-bound).
+struct FlowK {
+  double inv_dx, inv_dy, inv_4dx, inv_4dy;  // 1/dx, 1/dy, 1/(4 dx), 1/(4 dy)
+  double lim_x, lim_y;                      // dx/(4 dt), dy/(4 dt)
+  double dt_wi;                             // dt / wi
+  double gamma;
+};
+inline FlowK flow_constants(double dt, double dx, double dy, double wi, double gamma) {
+  return {1.0 / dx, 1.0 / dy, 1.0 / (4.0 * dx), 1.0 / (4.0 * dy), dx / (4.0 * dt), dy / (4.0 * dt), dt / wi, gamma};
 }
 // One sub-step, LDS-tiled: a workgroup owns kFlowTX columns x kFlowRows rows
 // and walks down its strip with a three-row ring of (s, H) in LDS (one halo
@@ -715,12 +726,16 @@ __device__ __forceinline__ double flow_face_q(double Ha, double Hb, double gn, d
 // becomes the next row's north face.  A face shared by two workgroups (or two
 // shards) is computed by both from the same values in the same order, so they
 // agree bit for bit (restatement: tests/harness.py:ice_flow_step_restated).
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
+// accesses, not for its global loads and stores (a __syncthreads() fence would
+// drain them, and with them the rows prefetched into registers).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // DMAX: instead of stepping, the largest face diffusivity of the workgroup's
 // faces goes to out[workgroup] (the CFL bound of tfg_ice_flow_dmax).
-constexpr int kFlowTX = 256, kFlowRows = 32;
+constexpr int kFlowTX = 256, kFlowRows = 32, kFlowPF = 1;  // kFlowPF rows of loads in flight (2 and 4 measured slower)
 template <class R, bool DMAX>
-__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, double dx, double dy, double dt, double gamma,
-                                                      double* __restrict__ out) {
+__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out) {
 #pragma clang fp contract(off)
   __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], qx[kFlowTX + 1];
   double dmax = 0.0;
@@ -729,54 +744,96 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, double d
   const int64_t r0 = (int64_t)blockIdx.y * kFlowRows;
   const int64_t r1 = r0 + kFlowRows < g.ny ? r0 + kFlowRows : g.ny;
   const int64_t c = c0 + t;
-  auto slot = [&](int64_t rr) { return (int)((rr - r0 + 1) % 3); };
-  auto load = [&](int64_t rr) {
+  auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) % 3; };  // 32-bit: rr - r0 + 1 <= kFlowRows + 1
+  // A row of (s, H) for columns c0-1 .. c0+kFlowTX, fetched into registers
+  // one row ahead and written to LDS a row later, so its HBM latency overlaps
+  // the current row's face arithmetic.  Raw values: (elev, h_iwe), or (s, H)
+  // from a halo row; a missing row outside the domain repeats the edge row.
+  struct Raw { double a[2], b[2]; bool halo; };
+  auto fetch = [&](int64_t rr, Raw& v) {
+    v.halo = (rr < 0 && g.hn) || (rr >= g.ny && g.hs);
+    const double* hr = rr < 0 ? g.hn : g.hs;
+    const int64_t rc_ = rr < 0 ? 0 : (rr >= g.ny ? g.ny - 1 : rr);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = t + j * kFlowTX;
+      if (k < kFlowTX + 2) {
+        const int64_t cc = c0 - 1 + k;
+        const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
+        if (v.halo) {
+          v.a[j] = hr[cl];
+          v.b[j] = hr[g.nx + cl];
+        } else {
+          v.a[j] = (double)static_cast<const R*>(g.elev)[rc_ * g.nx + cl];
+          v.b[j] = g.iwe[rc_ * g.nx + cl];
+        }
+      }
+    }
+  };
+  auto put = [&](int64_t rr, const Raw& v) {
     const int sl = slot(rr);
-    const bool no_row = (rr < 0 && !g.hn) || (rr >= g.ny && !g.hs);
-    for (int k = t; k < kFlowTX + 2; k += kFlowTX) {
-      const int64_t cc = c0 - 1 + k;
-      sS[sl][k] = flow_S<R>(g, rr, cc);
-      const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
-      sH[sl][k] = no_row ? 0.0 : flow_H<R>(g, rr, cl);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = t + j * kFlowTX;
+      if (k < kFlowTX + 2) {
+        sS[sl][k] = v.halo ? v.a[j] : v.a[j] + v.b[j] * g.wi;
+        sH[sl][k] = v.halo ? v.b[j] : v.b[j] * g.wi;
+      }
     }
   };
   auto face_y = [&](int a, int b) {  // between the rows in slots a (north) and b (south), column c
-    const double gn = (sS[b][t + 1] - sS[a][t + 1]) / dy;
-    const double gt = ((sS[a][t + 2] - sS[a][t]) + (sS[b][t + 2] - sS[b][t])) / (4.0 * dx);
+    const double gn = (sS[b][t + 1] - sS[a][t + 1]) * K.inv_dy;
+    const double gt = ((sS[a][t + 2] - sS[a][t]) + (sS[b][t + 2] - sS[b][t])) * K.inv_4dx;
     if constexpr (DMAX) {
-      if (c < g.nx) dmax = fmax(dmax, flow_face_D(sH[a][t + 1], sH[b][t + 1], gn, gt, gamma));
+      if (c < g.nx) dmax = fmax(dmax, flow_face_D(sH[a][t + 1], sH[b][t + 1], gn, gt, K.gamma));
       return 0.0;
     }
-    return flow_face_q(sH[a][t + 1], sH[b][t + 1], gn, gt, gamma, dy, dt);
+    return flow_face_q(sH[a][t + 1], sH[b][t + 1], gn, gt, K.gamma, K.lim_y);
   };
-  load(r0 - 1);
-  load(r0);
+  // rows r0-1 and r0 first; rows r0+1 .. r0+kFlowPF in flight in registers
+  {
+    Raw v;
+    fetch(r0 - 1, v);
+    put(r0 - 1, v);
+    fetch(r0, v);
+    put(r0, v);
+  }
+  Raw buf[kFlowPF];
+#pragma unroll
+  for (int j = 0; j < kFlowPF; ++j)
+    if (r0 + 1 + j <= r1) fetch(r0 + 1 + j, buf[j]);
   double qN = 0.0;
-  for (int64_t r = r0; r < r1; ++r) {
-    __syncthreads();  // row r-2's slot and qx are free
-    load(r + 1);
-    __syncthreads();
-    const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
-    for (int k = t; k < kFlowTX + 1; k += kFlowTX) {  // x-faces between columns c0-1+k and c0+k
-      const int64_t fc = c0 - 1 + k;
-      double q = 0.0;
-      if (fc >= 0 && fc + 1 < g.nx) {
-        const double gn = (sS[rc][k + 1] - sS[rc][k]) / dx;
-        const double gt = ((sS[rp][k] - sS[rm][k]) + (sS[rp][k + 1] - sS[rm][k + 1])) / (4.0 * dy);
-        if constexpr (DMAX) dmax = fmax(dmax, flow_face_D(sH[rc][k], sH[rc][k + 1], gn, gt, gamma));
-        else q = flow_face_q(sH[rc][k], sH[rc][k + 1], gn, gt, gamma, dx, dt);
+  for (int64_t rb = r0; rb < r1; rb += kFlowPF) {
+#pragma unroll
+    for (int jj = 0; jj < kFlowPF; ++jj) {
+      const int64_t r = rb + jj;
+      if (r >= r1) break;
+      lds_barrier();  // row r-2's slot and qx are free
+      put(r + 1, buf[jj]);
+      if (r + 1 + kFlowPF <= r1) fetch(r + 1 + kFlowPF, buf[jj]);  // in flight for the next kFlowPF rows
+      lds_barrier();
+      const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
+      for (int k = t; k < kFlowTX + 1; k += kFlowTX) {  // x-faces between columns c0-1+k and c0+k
+        const int64_t fc = c0 - 1 + k;
+        double q = 0.0;
+        if (fc >= 0 && fc + 1 < g.nx) {
+          const double gn = (sS[rc][k + 1] - sS[rc][k]) * K.inv_dx;
+          const double gt = ((sS[rp][k] - sS[rm][k]) + (sS[rp][k + 1] - sS[rm][k + 1])) * K.inv_4dy;
+          if constexpr (DMAX) dmax = fmax(dmax, flow_face_D(sH[rc][k], sH[rc][k + 1], gn, gt, K.gamma));
+          else q = flow_face_q(sH[rc][k], sH[rc][k + 1], gn, gt, K.gamma, K.lim_x);
+        }
+        qx[k] = q;
       }
-      qx[k] = q;
+      if (r == r0) qN = (r > 0 || g.hn) ? face_y(rm, rc) : 0.0;
+      const double qS = (r + 1 < g.ny || g.hs) ? face_y(rc, rp) : 0.0;
+      lds_barrier();  // qx complete
+      if (!DMAX && c < g.nx) {
+        const int64_t i = r * g.nx + c;
+        const double div = (qx[t + 1] - qx[t]) * K.inv_dx + (qS - qN) * K.inv_dy;
+        out[i] = fmax(g.iwe[i] - K.dt_wi * div, 0.0);
+      }
+      qN = qS;
     }
-    if (r == r0) qN = (r > 0 || g.hn) ? face_y(rm, rc) : 0.0;
-    const double qS = (r + 1 < g.ny || g.hs) ? face_y(rc, rp) : 0.0;
-    __syncthreads();  // qx complete
-    if (!DMAX && c < g.nx) {
-      const int64_t i = r * g.nx + c;
-      const double div = (qx[t + 1] - qx[t]) / dx + (qS - qN) / dy;
-      out[i] = fmax(g.iwe[i] - (dt / g.wi) * div, 0.0);
-    }
-    qN = qS;
   }
   if constexpr (DMAX) {
     __syncthreads();
@@ -1825,11 +1882,12 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
   const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
   if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
   const int64_t gb = (int64_t)fgrid.x * fgrid.y;
+  const FlowK fk = flow_constants(1.0, dx, dy, h->dp.wi, h->flow_gamma);  // dt unused by the bound
   if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)gb * 8));  // the grid never changes
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, 1.0, h->flow_gamma, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red);
   else
-    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, 1.0, h->flow_gamma, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red);
   HIPCHK(h, hipGetLastError());
   std::vector<double> bm(gb);
   HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1850,10 +1908,11 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
   const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
   if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
+  const FlowK fk = flow_constants(dt_years, dx, dy, h->dp.wi, h->flow_gamma);
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+    hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp);
   else
-    hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, dx, dy, dt_years, h->flow_gamma, h->wtmp);
+    hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp);
   HIPCHK(h, hipGetLastError());
   hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
