@@ -281,9 +281,17 @@ int tfg_ice_flow_edges(tfg_handle* h, double* first, double* last, int on_device
  * sets the stable sub-step dt <= min(dx, dy)^2 / (4 D). */
 int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_north, const double* halo_south,
                       int halo_on_device, double* dmax);
-/* One explicit sub-step of dt_years. */
+/* One explicit sub-step of dt_years.  `part` splits it so a sharded caller
+ * can overlap its halo exchange with the interior rows:
+ *   TFG_FLOW_ALL       the whole sub-step (blocking);
+ *   TFG_FLOW_INTERIOR  the rows that read no halo row, queued asynchronously
+ *                      (pass no halos); it must be followed by
+ *   TFG_FLOW_EDGES     the rows next to the halos, then the commit (blocking).
+ * The sub-step reads the pre-step state throughout, so ALL == INTERIOR + EDGES
+ * bit for bit. */
+enum { TFG_FLOW_ALL = 0, TFG_FLOW_INTERIOR = 1, TFG_FLOW_EDGES = 2 };
 int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
-                      const double* halo_south, int halo_on_device);
+                      const double* halo_south, int halo_on_device, int part);
 
 /* Last error message of a handle (NULL: the last create/global error). */
 const char* tfg_last_error(const tfg_handle* h);

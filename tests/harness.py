@@ -394,7 +394,9 @@ class RestatedFlowShard:
     def ice_flow_dmax(self, dx, dy, north=None, south=None):
         return ice_flow_dmax_restated(self.elev, self.iwe, self.wi, self.gamma, dx, dy, north, south)
 
-    def ice_flow_step(self, dt, dx, dy, north=None, south=None):
+    def ice_flow_step(self, dt, dx, dy, north=None, south=None, part=0):
+        if part == 1:  # FLOW_INTERIOR: the restatement steps whole shards (in the FLOW_EDGES call)
+            return
         self.iwe = ice_flow_step_restated(self.elev, self.iwe, self.wi, self.gamma, dx, dy, dt, north, south)
 
 

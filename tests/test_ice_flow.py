@@ -87,6 +87,29 @@ def test_gpu_flow_step_matches_restatement(engine):
 
 
 @pytest.mark.gpu
+def test_gpu_flow_interior_then_edges_equals_whole_step():
+    """TFG_FLOW_INTERIOR + TFG_FLOW_EDGES (the overlapped sharded sub-step)
+    equals TFG_FLOW_ALL and the restatement bit for bit (7 row strips)."""
+    from topoflow_glacier import _native as nat
+
+    g = ice_flow_gamma(BASE_CFG)
+    bed, iwe = glacier_valley(230, 300)
+    b, w = bed[10:210], iwe[10:210]
+    north = np.stack([bed[9] + iwe[9] * WI, iwe[9] * WI])
+    south = np.stack([bed[210] + iwe[210] * WI, iwe[210] * WI])
+    want = ice_flow_step_restated(b, w, WI, g, DX, DY, 0.001, north, south)
+    for parts in ((nat.FLOW_ALL,), (nat.FLOW_INTERIOR, nat.FLOW_EDGES)):
+        e = _engine(b, w)
+        try:
+            for part in parts:
+                halos = (None, None) if part == nat.FLOW_INTERIOR else (north, south)
+                e.ice_flow_step(0.001, DX, DY, *halos, part=part)
+            np.testing.assert_array_equal(e.get_field("h_iwe").reshape(w.shape), want)
+        finally:
+            e.close()
+
+
+@pytest.mark.gpu
 def test_gpu_flow_year_conserves_and_matches_restatement():
     g = ice_flow_gamma(BASE_CFG)
     bed, iwe = glacier_valley(64, 48)
@@ -104,7 +127,7 @@ def test_gpu_flow_year_conserves_and_matches_restatement():
 
 @pytest.mark.gpu
 def test_gpu_sharded_flow_gloo_world2_equals_whole_grid(tmp_path):
-    ny, nx, tenths = 41, 30, 5
+    ny, nx, tenths = 150, 30, 5  # 75 rows per rank: 3 strips, so the interior part overlaps the swap
     ranks = _torchrun("gpu_flow", tmp_path, ny=ny, nx=nx, steps=tenths)
     bed, iwe = glacier_valley(ny, nx)
     e = _engine(bed, iwe)

@@ -735,13 +735,14 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // faces goes to out[workgroup] (the CFL bound of tfg_ice_flow_dmax).
 constexpr int kFlowTX = 256, kFlowRows = 32, kFlowPF = 1;  // kFlowPF rows of loads in flight (2 and 4 measured slower)
 template <class R, bool DMAX>
-__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out) {
+__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
+                                                      int strip0, int strip_step) {
 #pragma clang fp contract(off)
   __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], qx[kFlowTX + 1];
   double dmax = 0.0;
   const int t = threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.x * kFlowTX;
-  const int64_t r0 = (int64_t)blockIdx.y * kFlowRows;
+  const int64_t r0 = ((int64_t)strip0 + (int64_t)blockIdx.y * strip_step) * kFlowRows;  // this workgroup's strip
   const int64_t r1 = r0 + kFlowRows < g.ny ? r0 + kFlowRows : g.ny;
   const int64_t c = c0 + t;
   auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) % 3; };  // 32-bit: rr - r0 + 1 <= kFlowRows + 1
@@ -1885,9 +1886,9 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
   const FlowK fk = flow_constants(1.0, dx, dy, h->dp.wi, h->flow_gamma);  // dt unused by the bound
   if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)gb * 8));  // the grid never changes
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1);
   else
-    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red);
+    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1);
   HIPCHK(h, hipGetLastError());
   std::vector<double> bm(gb);
   HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1899,21 +1900,34 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
 }
 
 int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
-                      const double* halo_south, int halo_on_device) {
+                      const double* halo_south, int halo_on_device, int part) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0) || !(dt_years > 0)) return fail(h, TFG_ERR_ARG, "dt, dx and dy must be > 0");
+  if (part != TFG_FLOW_ALL && part != TFG_FLOW_INTERIOR && part != TFG_FLOW_EDGES)
+    return fail(h, TFG_ERR_ARG, "part must be TFG_FLOW_ALL, TFG_FLOW_INTERIOR or TFG_FLOW_EDGES");
+  if (part == TFG_FLOW_INTERIOR && (halo_north || halo_south))
+    return fail(h, TFG_ERR_ARG, "the interior part takes no halo rows");
   HIPCHK(h, hipSetDevice(h->device));
   FlowGrid g;
   if (int rc = flow_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
   if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
-  const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
-  if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
+  const int64_t strips = (h->ny + kFlowRows - 1) / kFlowRows;
+  if (strips > 65535) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
   const FlowK fk = flow_constants(dt_years, dx, dy, h->dp.wi, h->flow_gamma);
-  if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp);
-  else
-    hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp);
-  HIPCHK(h, hipGetLastError());
+  // strips [first, first + count*step) by `step`: all of them, the interior
+  // ones (no halo row read), or the first and last (the halo readers)
+  int first = 0, count = (int)strips, step = 1;
+  if (part == TFG_FLOW_INTERIOR) { first = 1; count = (int)std::max<int64_t>(strips - 2, 0); }
+  if (part == TFG_FLOW_EDGES) { count = strips > 1 ? 2 : 1; step = (int)std::max<int64_t>(strips - 1, 1); }
+  if (count > 0) {
+    const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)count);
+    if (h->engine == TFG_F32)
+      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step);
+    else
+      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step);
+    HIPCHK(h, hipGetLastError());
+  }
+  if (part == TFG_FLOW_INTERIOR) return TFG_OK;  // queued; the edges part commits
   hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -21,6 +21,7 @@ __all__ = [
 LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
 
 ABI_VERSION = 3  # include/tfg.h TFG_ABI_VERSION
+FLOW_ALL, FLOW_INTERIOR, FLOW_EDGES = 0, 1, 2  # tfg_ice_flow_step parts
 F32, F64, I32 = 0, 1, 2
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_DOMAIN = 0, 1, 2, 3, 4
 
@@ -110,7 +111,7 @@ def load() -> ctypes.CDLL:
         "tfg_terrain_from_dem": ([vp, ctypes.c_double, ctypes.c_double, vp, vp, i32, i32], i32),
         "tfg_ice_flow_edges": ([vp, dp, dp, i32], i32),
         "tfg_ice_flow_dmax": ([vp, ctypes.c_double, ctypes.c_double, dp, dp, i32, dp], i32),
-        "tfg_ice_flow_step": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32], i32),
+        "tfg_ice_flow_step": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32, i32], i32),
         "tfg_set_inputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),

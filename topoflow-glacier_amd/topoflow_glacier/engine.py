@@ -302,11 +302,13 @@ class GlacierEngine:
         self._chk(self.lib.tfg_ice_flow_dmax(self.h, float(dx), float(dy), pn, ps, 0, ctypes.byref(out)))
         return out.value
 
-    def ice_flow_step(self, dt_years: float, dx: float, dy: float, north=None, south=None) -> None:
-        """One explicit shallow-ice sub-step of dt_years (tfg_ice_flow_step)."""
+    def ice_flow_step(self, dt_years: float, dx: float, dy: float, north=None, south=None,
+                      part: int = nat.FLOW_ALL) -> None:
+        """One explicit shallow-ice sub-step of dt_years (tfg_ice_flow_step).
+        part: FLOW_ALL, or FLOW_INTERIOR (queued, no halos) then FLOW_EDGES."""
         kn, pn = self._halo_ptr(north, self.nx)
         ks, ps = self._halo_ptr(south, self.nx)
-        self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, 0))
+        self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, 0, int(part)))
 
     def ice_flow(self, dt_years: float, dx: float, dy: float, cfl: float = 0.5) -> int:
         """Move ice for dt_years on this shard alone (domain edges all round),

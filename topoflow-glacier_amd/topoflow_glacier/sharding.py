@@ -116,16 +116,18 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
     if on and dist.get_backend(group) == "nccl":
         dev = f"cuda:{torch.cuda.current_device()}"
 
-    def halos():
-        if not on:
-            return None, None
-        first, last = eng.ice_flow_edges()
+    FLOW_INTERIOR, FLOW_EDGES = 1, 2  # tfg_ice_flow_step parts (include/tfg.h)
+
+    def swap(first, last):
         n, s = exchange_halo_rows(torch.from_numpy(first.reshape(-1)).to(dev),
                                   torch.from_numpy(last.reshape(-1)).to(dev), group)
         if dev != "cpu":
             torch.cuda.current_stream().synchronize()
         return (None if n is None else n.cpu().numpy().reshape(2, -1),
                 None if s is None else s.cpu().numpy().reshape(2, -1))
+
+    def halos():
+        return swap(*eng.ice_flow_edges()) if on else (None, None)
 
     north, south = halos()
     dmax = float(eng.ice_flow_dmax(dx, dy, north, south))
@@ -139,8 +141,14 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
     n_sub = max(1, math.ceil(dt_years / dt_stable))
     if n_sub > max_substeps:
         raise ValueError(f"ice flow needs {n_sub} sub-steps (> {max_substeps}); shorten the interval")
+    dt = dt_years / n_sub
     for k in range(n_sub):
-        if k:
-            north, south = halos()
-        eng.ice_flow_step(dt_years / n_sub, dx, dy, north, south)
+        if k == 0 or not on:
+            eng.ice_flow_step(dt, dx, dy, north, south)  # halos of the CFL pass are current
+            continue
+        # the interior rows run on the GPU while the halo rows cross between ranks
+        first, last = eng.ice_flow_edges()
+        eng.ice_flow_step(dt, dx, dy, part=FLOW_INTERIOR)
+        north, south = swap(first, last)
+        eng.ice_flow_step(dt, dx, dy, north, south, part=FLOW_EDGES)
     return n_sub
