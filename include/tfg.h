@@ -292,6 +292,11 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
 enum { TFG_FLOW_ALL = 0, TFG_FLOW_INTERIOR = 1, TFG_FLOW_EDGES = 2 };
 int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
                       const double* halo_south, int halo_on_device, int part);
+/* n_sub sub-steps of dt_years / n_sub on an unsharded grid (no halos), in one
+ * blocking call: the sub-steps alternate between the state plane and a
+ * scratch plane, so no per-sub-step commit pass is needed.  Equals n_sub
+ * tfg_ice_flow_step calls bit for bit. */
+int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n_sub);
 
 /* Last error message of a handle (NULL: the last create/global error). */
 const char* tfg_last_error(const tfg_handle* h);

@@ -110,6 +110,29 @@ def test_gpu_flow_interior_then_edges_equals_whole_step():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n_sub", [4, 5])
+def test_gpu_flow_run_equals_sub_steps(n_sub):
+    """tfg_ice_flow_run (sub-steps ping-pong between state and scratch planes)
+    equals n_sub separate tfg_ice_flow_step calls bit for bit, h_ice included."""
+    bed, iwe = glacier_valley(100, 70)
+    got = []
+    for run in (True, False):
+        e = _engine(bed, iwe)
+        try:
+            if run:
+                e.ice_flow_run(0.01, DX, DY, n_sub)
+            else:
+                for _ in range(n_sub):
+                    e.ice_flow_step(0.01 / n_sub, DX, DY)
+            got.append((e.get_field("h_iwe"), e.get_field("h_ice")))
+        finally:
+            e.close()
+    for a, b in zip(*got):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(got[0][1], got[0][0] * WI)
+
+
+@pytest.mark.gpu
 def test_gpu_flow_year_conserves_and_matches_restatement():
     g = ice_flow_gamma(BASE_CFG)
     bed, iwe = glacier_valley(64, 48)

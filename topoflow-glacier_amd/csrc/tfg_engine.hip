@@ -736,7 +736,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 constexpr int kFlowTX = 256, kFlowRows = 32, kFlowPF = 1;  // kFlowPF rows of loads in flight (2 and 4 measured slower)
 template <class R, bool DMAX>
 __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
-                                                      int strip0, int strip_step) {
+                                                      int strip0, int strip_step, double* __restrict__ out_ice) {
 #pragma clang fp contract(off)
   __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], qx[kFlowTX + 1];
   double dmax = 0.0;
@@ -831,7 +831,9 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const Fl
       if (!DMAX && c < g.nx) {
         const int64_t i = r * g.nx + c;
         const double div = (qx[t + 1] - qx[t]) * K.inv_dx + (qS - qN) * K.inv_dy;
-        out[i] = fmax(g.iwe[i] - K.dt_wi * div, 0.0);
+        const double v = fmax(g.iwe[i] - K.dt_wi * div, 0.0);
+        out[i] = v;
+        if (out_ice) out_ice[i] = v * g.wi;  // writing the state plane: h_ice too (:1726)
       }
       qN = qS;
     }
@@ -1886,9 +1888,9 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
   const FlowK fk = flow_constants(1.0, dx, dy, h->dp.wi, h->flow_gamma);  // dt unused by the bound
   if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)gb * 8));  // the grid never changes
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1);
+    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr);
   else
-    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1);
+    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr);
   HIPCHK(h, hipGetLastError());
   std::vector<double> bm(gb);
   HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1922,13 +1924,46 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   if (count > 0) {
     const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)count);
     if (h->engine == TFG_F32)
-      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step);
+      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, nullptr);
     else
-      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step);
+      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, nullptr);
     HIPCHK(h, hipGetLastError());
   }
   if (part == TFG_FLOW_INTERIOR) return TFG_OK;  // queued; the edges part commits
   hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n_sub) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!(dx > 0) || !(dy > 0) || !(dt_years > 0) || n_sub < 1) return fail(h, TFG_ERR_ARG, "dt, dx, dy and n_sub must be > 0");
+  HIPCHK(h, hipSetDevice(h->device));
+  FlowGrid g;
+  if (int rc = flow_setup(h, nullptr, nullptr, 0, g)) return rc;
+  if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
+  const int64_t strips = (h->ny + kFlowRows - 1) / kFlowRows;
+  if (strips > 65535) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
+  const FlowK fk = flow_constants(dt_years / n_sub, dx, dy, h->dp.wi, h->flow_gamma);
+  const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)strips);
+  // ping-pong between the state plane and the scratch plane: a sub-step that
+  // lands in the state plane writes h_ice with it, so only an odd count needs
+  // the commit pass at the end
+  double* plane = h->st + S_HIWE * h->n_pad;
+  double* ice = h->st + S_HICE * h->n_pad;
+  for (int k = 0; k < n_sub; ++k) {
+    const bool to_state = (k & 1) != 0;
+    g.iwe = to_state ? h->wtmp : plane;
+    double* dst = to_state ? plane : h->wtmp;
+    if (h->engine == TFG_F32)
+      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, dst, 0, 1, to_state ? ice : nullptr);
+    else
+      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, dst, 0, 1, to_state ? ice : nullptr);
+    HIPCHK(h, hipGetLastError());
+  }
+  if (n_sub & 1)
+    hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;

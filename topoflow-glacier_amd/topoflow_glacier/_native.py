@@ -112,6 +112,7 @@ def load() -> ctypes.CDLL:
         "tfg_ice_flow_edges": ([vp, dp, dp, i32], i32),
         "tfg_ice_flow_dmax": ([vp, ctypes.c_double, ctypes.c_double, dp, dp, i32, dp], i32),
         "tfg_ice_flow_step": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32, i32], i32),
+        "tfg_ice_flow_run": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, i32], i32),
         "tfg_set_inputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),
@@ -143,6 +144,6 @@ def exported_symbols() -> list[str]:
         "tfg_abi_version", "tfg_build_info", "tfg_device_count", "tfg_create", "tfg_destroy",
         "tfg_set_stream", "tfg_get_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
-        "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_set_inputs", "tfg_get_outputs",
+        "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update",
     ) if hasattr(L, n)]

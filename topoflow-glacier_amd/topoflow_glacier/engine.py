@@ -310,6 +310,11 @@ class GlacierEngine:
         ks, ps = self._halo_ptr(south, self.nx)
         self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, 0, int(part)))
 
+    def ice_flow_run(self, dt_years: float, dx: float, dy: float, n_sub: int) -> None:
+        """n_sub sub-steps of dt_years / n_sub on this shard alone, in one call
+        (tfg_ice_flow_run: no per-sub-step commit pass)."""
+        self._chk(self.lib.tfg_ice_flow_run(self.h, float(dt_years), float(dx), float(dy), int(n_sub)))
+
     def ice_flow(self, dt_years: float, dx: float, dy: float, cfl: float = 0.5) -> int:
         """Move ice for dt_years on this shard alone (domain edges all round),
         in as many stable sub-steps as needed; returns the sub-step count."""

@@ -141,6 +141,9 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
     n_sub = max(1, math.ceil(dt_years / dt_stable))
     if n_sub > max_substeps:
         raise ValueError(f"ice flow needs {n_sub} sub-steps (> {max_substeps}); shorten the interval")
+    if not on and hasattr(eng, "ice_flow_run"):
+        eng.ice_flow_run(dt_years, dx, dy, n_sub)  # one shard: sub-steps ping-pong on the device
+        return n_sub
     dt = dt_years / n_sub
     for k in range(n_sub):
         if k == 0 or not on:
