@@ -110,6 +110,31 @@ def test_gpu_flow_interior_then_edges_equals_whole_step():
 
 
 @pytest.mark.gpu
+def test_gpu_flow_device_halos_equal_host_halos():
+    """Halo rows handed over as CUDA tensors (the RCCL path: edges written by
+    the engine into device tensors, read back by device pointer) give the same
+    sub-step as host arrays."""
+    import torch
+
+    bed, iwe = glacier_valley(200, 90)
+    top = _engine(bed[:100], iwe[:100])
+    bot = _engine(bed[100:], iwe[100:], row0=100)
+    try:
+        _, last_h = top.ice_flow_edges()
+        first_d, _ = bot.ice_flow_edges(device="cuda:0")
+        _, last_d = top.ice_flow_edges(device="cuda:0")
+        np.testing.assert_array_equal(last_d.cpu().numpy(), last_h)
+        want = ice_flow_step_restated(bed[100:], iwe[100:], WI, ice_flow_gamma(BASE_CFG), DX, DY, 0.001, last_h, None)
+        assert bot.ice_flow_dmax(DX, DY, last_d, None) == bot.ice_flow_dmax(DX, DY, last_h, None)
+        bot.ice_flow_step(0.001, DX, DY, last_d * 1.0, None)  # a fresh tensor from a torch kernel
+        np.testing.assert_array_equal(bot.get_field("h_iwe").reshape(100, 90), want)
+        assert first_d.is_cuda and torch.isfinite(first_d).all()
+    finally:
+        top.close()
+        bot.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n_sub", [4, 5])
 def test_gpu_flow_run_equals_sub_steps(n_sub):
     """tfg_ice_flow_run (sub-steps ping-pong between state and scratch planes)

@@ -280,35 +280,69 @@ class GlacierEngine:
 
     # -- optional lateral ice flow (tfg_ice_flow_*, off unless called) -----------------
     @staticmethod
-    def _halo_ptr(halo, nx):
-        if halo is None:
-            return None, None
-        a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(2, nx))
-        return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
-
-    def ice_flow_edges(self) -> tuple[np.ndarray, np.ndarray]:
-        """This shard's first and last rows as ice-flow halo rows, [2][nx] each
-        (surface elevation, ice thickness)."""
-        first, last = np.empty((2, self.nx)), np.empty((2, self.nx))
+    def _halo_args(north, south, nx):
+        """Halo rows as (keep-alive, north ptr, south ptr, on_device): numpy
+        arrays (host) or torch CUDA tensors (device, e.g. straight from an RCCL
+        receive), [2][nx] fp64 each, or None at the domain edge."""
+        keep, ptrs, dev = [], [], set()
         dp = ctypes.POINTER(ctypes.c_double)
+        for halo in (north, south):
+            if halo is None:
+                ptrs.append(None)
+            elif getattr(halo, "is_cuda", False):
+                import torch
+
+                t = halo.reshape(-1).to(torch.float64).contiguous()
+                if t.numel() != 2 * nx:
+                    raise ValueError(f"halo rows need [2][{nx}] values")
+                keep.append(t)
+                ptrs.append(ctypes.cast(ctypes.c_void_p(t.data_ptr()), dp))
+                dev.add(1)
+            else:
+                a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(2, nx))
+                keep.append(a)
+                ptrs.append(a.ctypes.data_as(dp))
+                dev.add(0)
+        if len(dev) > 1:
+            raise ValueError("halo rows must be both host arrays or both device tensors")
+        if 1 in dev:
+            import torch
+
+            torch.cuda.current_stream().synchronize()  # the tensors' producer (RCCL, a cast) is done
+        return keep, ptrs[0], ptrs[1], int(1 in dev)
+
+    def ice_flow_edges(self, device=None):
+        """This shard's first and last rows as ice-flow halo rows, [2][nx]
+        each (surface elevation, ice thickness): numpy arrays, or torch CUDA
+        tensors when `device` is given (ready for an RCCL exchange)."""
+        dp = ctypes.POINTER(ctypes.c_double)
+        if device is not None:
+            import torch
+
+            first = torch.empty((2, self.nx), dtype=torch.float64, device=device)
+            last = torch.empty((2, self.nx), dtype=torch.float64, device=device)
+            torch.cuda.current_stream(first.device).synchronize()
+            self._chk(self.lib.tfg_ice_flow_edges(self.h, ctypes.cast(ctypes.c_void_p(first.data_ptr()), dp),
+                                                  ctypes.cast(ctypes.c_void_p(last.data_ptr()), dp), 1))
+            return first, last  # tfg_ice_flow_edges synchronises the engine stream before returning
+        first, last = np.empty((2, self.nx)), np.empty((2, self.nx))
         self._chk(self.lib.tfg_ice_flow_edges(self.h, first.ctypes.data_as(dp), last.ctypes.data_as(dp), 0))
         return first, last
 
     def ice_flow_dmax(self, dx: float, dy: float, north=None, south=None) -> float:
         """Largest face diffusivity [m2 yr-1] (sets the stable sub-step)."""
-        kn, pn = self._halo_ptr(north, self.nx)
-        ks, ps = self._halo_ptr(south, self.nx)
+        keep, pn, ps, on_dev = self._halo_args(north, south, self.nx)
         out = ctypes.c_double()
-        self._chk(self.lib.tfg_ice_flow_dmax(self.h, float(dx), float(dy), pn, ps, 0, ctypes.byref(out)))
+        self._chk(self.lib.tfg_ice_flow_dmax(self.h, float(dx), float(dy), pn, ps, on_dev, ctypes.byref(out)))
         return out.value
 
     def ice_flow_step(self, dt_years: float, dx: float, dy: float, north=None, south=None,
                       part: int = nat.FLOW_ALL) -> None:
         """One explicit shallow-ice sub-step of dt_years (tfg_ice_flow_step).
         part: FLOW_ALL, or FLOW_INTERIOR (queued, no halos) then FLOW_EDGES."""
-        kn, pn = self._halo_ptr(north, self.nx)
-        ks, ps = self._halo_ptr(south, self.nx)
-        self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, 0, int(part)))
+        keep, pn, ps, on_dev = self._halo_args(north, south, self.nx)
+        self._chk(self.lib.tfg_ice_flow_step(self.h, float(dt_years), float(dx), float(dy), pn, ps, on_dev, int(part)))
+        del keep
 
     def ice_flow_run(self, dt_years: float, dx: float, dy: float, n_sub: int) -> None:
         """n_sub sub-steps of dt_years / n_sub on this shard alone, in one call

@@ -118,16 +118,21 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
 
     FLOW_INTERIOR, FLOW_EDGES = 1, 2  # tfg_ice_flow_step parts (include/tfg.h)
 
+    # On the GPU path the halo rows never leave the devices: the engine writes
+    # its edge rows into CUDA tensors, RCCL swaps them over xGMI, and the
+    # engine reads the received tensors by device pointer.
+    def edges():
+        return eng.ice_flow_edges(device=dev) if dev != "cpu" else eng.ice_flow_edges()
+
     def swap(first, last):
-        n, s = exchange_halo_rows(torch.from_numpy(first.reshape(-1)).to(dev),
-                                  torch.from_numpy(last.reshape(-1)).to(dev), group)
+        t = (lambda a: a.reshape(-1)) if dev != "cpu" else (lambda a: torch.from_numpy(a.reshape(-1)))
+        n, s = exchange_halo_rows(t(first), t(last), group)
         if dev != "cpu":
-            torch.cuda.current_stream().synchronize()
-        return (None if n is None else n.cpu().numpy().reshape(2, -1),
-                None if s is None else s.cpu().numpy().reshape(2, -1))
+            return n, s  # device tensors; the engine orders its copy after torch's stream
+        return (None if n is None else n.numpy().reshape(2, -1), None if s is None else s.numpy().reshape(2, -1))
 
     def halos():
-        return swap(*eng.ice_flow_edges()) if on else (None, None)
+        return swap(*edges()) if on else (None, None)
 
     north, south = halos()
     dmax = float(eng.ice_flow_dmax(dx, dy, north, south))
@@ -150,7 +155,7 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
             eng.ice_flow_step(dt, dx, dy, north, south)  # halos of the CFL pass are current
             continue
         # the interior rows run on the GPU while the halo rows cross between ranks
-        first, last = eng.ice_flow_edges()
+        first, last = edges()
         eng.ice_flow_step(dt, dx, dy, part=FLOW_INTERIOR)
         north, south = swap(first, last)
         eng.ice_flow_step(dt, dx, dy, north, south, part=FLOW_EDGES)
