@@ -738,7 +738,7 @@ template <class R, bool DMAX>
 __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
                                                       int strip0, int strip_step, double* __restrict__ out_ice) {
 #pragma clang fp contract(off)
-  __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], qx[kFlowTX + 1];
+  __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], sW[3][kFlowTX + 2], qx[kFlowTX + 1];  // sW: h_iwe as read
   double dmax = 0.0;
   const int t = threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.x * kFlowTX;
@@ -779,6 +779,7 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const Fl
       if (k < kFlowTX + 2) {
         sS[sl][k] = v.halo ? v.a[j] : v.a[j] + v.b[j] * g.wi;
         sH[sl][k] = v.halo ? v.b[j] : v.b[j] * g.wi;
+        sW[sl][k] = v.b[j];  // h_iwe of an in-domain row (the only rows a workgroup updates)
       }
     }
   };
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const Fl
       if (!DMAX && c < g.nx) {
         const int64_t i = r * g.nx + c;
         const double div = (qx[t + 1] - qx[t]) * K.inv_dx + (qS - qN) * K.inv_dy;
-        const double v = fmax(g.iwe[i] - K.dt_wi * div, 0.0);
+        const double v = fmax(sW[rc][t + 1] - K.dt_wi * div, 0.0);
         out[i] = v;
         if (out_ice) out_ice[i] = v * g.wi;  // writing the state plane: h_ice too (:1726)
       }
