@@ -207,6 +207,23 @@ def test_fp64_synthetic_vs_oracle():
     assert rep["max_rel"] <= 1e-10, rep["summary"]
 
 
+@pytest.mark.parametrize("engine,tol", [("float32", None), ("float64", 1e-10)])
+def test_quarter_hour_steps_vs_oracle(engine, tol):
+    """BASELINE config 5's time step: dt = 0.25 h, a 288-slot snowfall window,
+    100 steps (longer than the window, so slots expire), fused 24 per launch."""
+    rep = run_gpu_vs_oracle(16, 48, 100, engine, seed=5, cfg_over={"dt": 0.25})
+    assert rep["ok"], rep["summary"]
+    if tol is not None:
+        assert rep["max_rel"] <= tol, rep["summary"]
+
+
+def test_satterlund_synthetic_vs_oracle():
+    """SATTERLUND: True (config.py:101) on a synthetic grid: the alternative
+    vapour-pressure and emissivity formulas (:784-796, :1190-1192) in fp32."""
+    rep = run_gpu_vs_oracle(16, 48, 48, "float32", seed=9, cfg_over={"SATTERLUND": True})
+    assert rep["ok"], rep["summary"]
+
+
 # ---------------------------------------------------------------- invariances
 @pytest.mark.parametrize("engine", ["float32", "float64"])
 def test_fusion_is_invisible(engine):
