@@ -196,7 +196,7 @@ def test_fp32_engine_vs_oracle_on_fixture_inputs(name):
         assert err <= 1e-5, v
 
 
-@pytest.mark.parametrize("shape,nsteps", [((32, 64), 48), ((17, 33), 30)])
+@pytest.mark.parametrize("shape,nsteps", [((32, 64), 48), ((17, 33), 30), ((1, 1), 30), ((3, 65), 30)])  # ragged: one cell, one wave + 1
 def test_fp32_synthetic_vs_oracle(shape, nsteps):
     rep = run_gpu_vs_oracle(shape[0], shape[1], nsteps, "float32", seed=11)
     assert rep["ok"], rep["summary"]
