@@ -562,6 +562,10 @@ def test_bmi_grid_mode_vs_oracle(tmp_path, ny, nx):
     names = {"P": "atmosphere_water__liquid_equivalent_precipitation_rate", "T_air": "land_surface_air__temperature",
              "Hum_sp": "atmosphere_air_water~vapor__relative_saturation", "P_air": "land_surface_air__pressure",
              "uz": "wind_speed_UV"}
+    # per-cell terrain through the additive static variables (the YAML scalars otherwise)
+    for v, bmi in (("elev", "land_surface__elevation"), ("slope", "land_surface__slope"),
+                   ("aspect", "land_surface__aspect_angle")):
+        model.set_value(bmi, syn[v].astype(np.float64))
     for k in range(nsteps):
         for v, bmi in names.items():
             model.set_value(bmi, syn[v][k % 24].astype(np.float64))
@@ -575,7 +579,7 @@ def test_bmi_grid_mode_vs_oracle(tmp_path, ny, nx):
     model.finalize()
     r32 = lambda a: np.asarray(a, dtype=np.float32).astype(np.float64)  # noqa: E731
     forcing = {v: r32(syn[v][np.arange(nsteps) % 24]) for v in names}
-    static = {"elev": np.full(n, cfg["elev"]), "slope": np.full(n, cfg["slope"]), "aspect": np.full(n, cfg["aspect"]),
+    static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"],
               "h0_snow": np.full(n, cfg["h0_snow"]), "h0_ice": np.full(n, cfg["h0_ice"]),
               "h0_swe": np.full(n, cfg["h0_swe"]), "h0_iwe": np.full(n, cfg["h0_iwe"])}
     static = {k: r32(v) if k in ("elev", "slope", "aspect") else v for k, v in static.items()}
@@ -585,3 +589,28 @@ def test_bmi_grid_mode_vs_oracle(tmp_path, ny, nx):
         assert err <= 1e-5, (v, err)
     for v in ("h_swe", "h_iwe"):
         assert parity(got[v], ref[v][-1])[0] <= 1e-5, v
+
+
+def test_bmi_static_rasters(tmp_path):
+    """The additive static variables: per-cell elev / slope / aspect through
+    set_value, readable back, absent from the reference's input list, and a
+    slope out of range fails update() like the reference (:1106-1111) until a
+    valid raster replaces it."""
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    model = BmiTopoflowGlacier()
+    model.initialize(str(_write_cfg(tmp_path, dict(BASE_CFG, ny=4, nx=5))))
+    assert "land_surface__slope" not in model.get_input_var_names()
+    assert model.get_var_units("land_surface__slope") == "m km-1"
+    np.testing.assert_array_equal(model.get_value("land_surface__elevation", np.zeros(20)), BASE_CFG["elev"])
+    slope = np.linspace(1.0, 90.0, 20)
+    model.set_value("land_surface__slope", slope)
+    np.testing.assert_array_equal(model.get_value("land_surface__slope", np.zeros(20)), slope)
+    model.update()
+    model.set_value_at_indices("land_surface__slope", [3], [-1.0])
+    with pytest.raises(AttributeError):
+        model.update()
+    model.set_value("land_surface__slope", slope)
+    model.update()
+    assert model.get_current_time() == 2 * model.get_time_step()
+    model.finalize()

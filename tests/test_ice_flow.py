@@ -219,7 +219,7 @@ def test_bmi_ice_flow_every_interval(tmp_path):
     for mode in ("update", "update_until"):
         m = BmiTopoflowGlacier()
         m.initialize(str(path))
-        m._engine.set_field("elev", bed.reshape(-1))
+        m.set_value("land_surface__elevation", bed.reshape(-1))
         m.set_value("glacier__liquid_equivalent_depth", iwe.reshape(-1))
         for name, v in (("land_surface_air__temperature", -5.0), ("land_surface_air__pressure", 88000.0),
                         ("atmosphere_air_water~vapor__relative_saturation", 0.003), ("wind_speed_UV", 3.0),

@@ -47,6 +47,19 @@ _dynamic_input_vars = [
     ("land_surface_air__temperature", "degC"),
     ("wind_speed_UV", "m sec-1"),
 ]
+# Additive, settable static rasters (not in the reference's var lists, which
+# stay unchanged): the YAML scalars elev / slope / aspect (config.py:19-28)
+# per cell, for gridded runs.  Units and meaning as the reference uses them:
+# slope is the tangent of the slope angle labelled m km-1 (:1095-1113), the
+# aspect in "degrees" enters the radians formula (:1082-1093).
+_static_vars = [
+    ("land_surface__elevation", "m"),
+    ("land_surface__slope", "m km-1"),
+    ("land_surface__aspect_angle", "deg"),
+]
+_STATIC_FIELD = {"land_surface__elevation": "elev", "land_surface__slope": "slope",
+                 "land_surface__aspect_angle": "aspect"}
+
 _output_vars = [
     ("snowpack__depth", "m"),
     ("snowpack__liquid-equivalent_depth", "m"),
@@ -150,6 +163,7 @@ class BmiTopoflowGlacier(BmiBase):
     def __init__(self) -> None:
         self._dynamic_inputs = build_context(_dynamic_input_vars)
         self._outputs = build_context(_output_vars)
+        self._static = build_context(_static_vars)
         self._timestep: int = 0
         self._engine: GlacierEngine | None = None
         self._stale: set[str] = set()
@@ -201,6 +215,10 @@ class BmiTopoflowGlacier(BmiBase):
         self.n_cells = n
         self._dynamic_inputs = build_context(_dynamic_input_vars, n)
         self._outputs = build_context(_output_vars, n)
+        self._static = build_context(_static_vars, n)
+        for name, key in (("land_surface__elevation", "elev"), ("land_surface__slope", "slope"),
+                          ("land_surface__aspect_angle", "aspect")):
+            self._static.set_value(name, np.float64(getattr(cfg, key)))
         self._eager = n <= _EAGER_MAX_CELLS
         self._in_block = np.empty((5, n), dtype=np.float64)
         self._out_block = np.empty((8, n), dtype=np.float64)
@@ -346,7 +364,7 @@ class BmiTopoflowGlacier(BmiBase):
         self._stale.discard(internal)
 
     def _mirror(self, external: str) -> np.ndarray:
-        ctx = first_containing(external, self._outputs, self._dynamic_inputs)
+        ctx = first_containing(external, self._outputs, self._dynamic_inputs, self._static)
         if ctx is self._outputs and self._engine is not None:
             internal = _int(external)
             if internal in self._stale:
@@ -369,8 +387,26 @@ class BmiTopoflowGlacier(BmiBase):
     def get_output_var_names(self) -> tuple[str, ...]:
         return tuple(self._outputs.names())
 
+    def _set_static(self, name: str) -> None:
+        """Push a static raster to the engine (additive _static_vars).  A slope
+        out of range is logged and makes update() fail, as at initialize()
+        (reference :1106-1111)."""
+        try:
+            self._engine.set_field(_STATIC_FIELD[name], self._static.value(name))
+            if name == "land_surface__slope":
+                self._beta_invalid = False
+        except nat.NativeError as e:
+            if e.code != nat.ERR_DOMAIN:
+                raise
+            logger.error("ERROR: In met_base.py, some slope angles are out of range.  Returning without setting beta.")
+            self._beta_invalid = True
+
     def set_value(self, name: str, src) -> None:
-        ctx = first_containing(name, self._outputs, self._dynamic_inputs)
+        if name in _STATIC_FIELD:
+            self._static.set_value(name, src)
+            self._set_static(name)
+            return
+        ctx = first_containing(name, self._outputs, self._dynamic_inputs, self._static)
         ctx.set_value(name, src)
         if ctx is self._outputs:
             internal = _int(name)
@@ -378,8 +414,12 @@ class BmiTopoflowGlacier(BmiBase):
             self._dirty_outputs.add(internal)
 
     def set_value_at_indices(self, name: str, inds, src) -> None:
+        if name in _STATIC_FIELD:
+            self._static.set_value_at_indices(name, np.asarray(inds), np.asarray(src))
+            self._set_static(name)
+            return
         self._mirror(name)  # refresh first so the untouched entries stay current
-        ctx = first_containing(name, self._outputs, self._dynamic_inputs)
+        ctx = first_containing(name, self._outputs, self._dynamic_inputs, self._static)
         ctx.set_value_at_indices(name, np.asarray(inds), np.asarray(src))
         if ctx is self._outputs:
             self._dirty_outputs.add(_int(name))
@@ -398,7 +438,7 @@ class BmiTopoflowGlacier(BmiBase):
 
     def get_value_at_indices(self, name: str, dest, inds):
         self._mirror(name)
-        return first_containing(name, self._outputs, self._dynamic_inputs).value_at_indices(name, dest, np.asarray(inds))
+        return first_containing(name, self._outputs, self._dynamic_inputs, self._static).value_at_indices(name, dest, np.asarray(inds))
 
     def get_var_itemsize(self, name: str) -> int:
         return self.get_value_ptr(name).itemsize
@@ -410,14 +450,14 @@ class BmiTopoflowGlacier(BmiBase):
         return str(self.get_value_ptr(name).dtype)
 
     def get_var_units(self, name: str) -> str:
-        return first_containing(name, self._outputs, self._dynamic_inputs).unit(name)
+        return first_containing(name, self._outputs, self._dynamic_inputs, self._static).unit(name)
 
     def get_var_grid(self, name: str) -> int:
-        first_containing(name, self._outputs, self._dynamic_inputs)
+        first_containing(name, self._outputs, self._dynamic_inputs, self._static)
         return 0
 
     def get_var_location(self, name: str) -> str:
-        first_containing(name, self._outputs, self._dynamic_inputs)
+        first_containing(name, self._outputs, self._dynamic_inputs, self._static)
         return "node"
 
     # ------------------------------------------------------------------ grid
