@@ -201,8 +201,14 @@ int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n
 int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
                int dst_dtype, int64_t n);
 
+/* `index` value for TFG_OUT_H_SNOW / TFG_OUT_H_ICE: the fp64 previous-step
+ * depth the next step reads (:895-911 uses the previous depths), rather than a
+ * history slot -- exact checkpoint / restart. */
+#define TFG_PREV_DEPTH (-1)
+
 /* Copy n cells of a field out.  `index` is the history slot for TFG_OUT_*
- * (except H_SWE/H_IWE, which are state), the frame for TFG_IN_*.
+ * (except H_SWE/H_IWE, which are state; TFG_PREV_DEPTH above), the frame for
+ * TFG_IN_*.
  * Replaces: get_value / get_value_ptr (:1810-1828). */
 int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n,
                   int dst_on_device);

@@ -1150,6 +1150,8 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
   if (!src) return fail(h, TFG_ERR_ARG, "null src");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n = " + std::to_string(n) + " != ny*nx = " + std::to_string(h->n));
   HIPCHK(h, hipSetDevice(h->device));
+  // setting a depth writes the previous-step depth the next step reads, so TFG_PREV_DEPTH is slot 0
+  if ((field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE) && index == TFG_PREV_DEPTH) index = 0;  // same as a plain depth set
   if (is_frame_field(field) && (index < 0 || index >= h->n_frames)) return fail(h, TFG_ERR_ARG, "frame index out of range");
   if (is_hist_field(field) && (index < 0 || index >= h->hist_depth)) return fail(h, TFG_ERR_ARG, "history slot out of range");
   if (field == TFG_ST_CATCH_ID) {
@@ -1223,6 +1225,16 @@ int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype,
   if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
   HIPCHK(h, hipSetDevice(h->device));
+  if ((field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE) && index == TFG_PREV_DEPTH) {
+    // the fp64 previous-step depth the next step reads (checkpoint / restart)
+    if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+    if (h->depths_derived) {
+      hipLaunchKernelGGL(k_materialise_depths, grid_for(h->n_pad), 256, 0, h->stream, h->st, h->n_pad, h->dp.ws, h->dp.wi);
+      HIPCHK(h, hipGetLastError());
+    }
+    return download(h, dst, dst_dtype, h->st + (field == TFG_OUT_H_SNOW ? S_HSNOW : S_HICE) * h->n_pad, TFG_F64, n,
+                    dst_on_device);
+  }
   if (is_frame_field(field) && (index < 0 || index >= h->n_frames)) return fail(h, TFG_ERR_ARG, "frame index out of range");
   if (is_hist_field(field) && (index < 0 || index >= h->hist_depth)) return fail(h, TFG_ERR_ARG, "history slot out of range");
   if (field == TFG_ST_CATCH_ID) {

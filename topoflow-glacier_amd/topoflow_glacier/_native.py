@@ -22,6 +22,7 @@ LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tf
 
 ABI_VERSION = 3  # include/tfg.h TFG_ABI_VERSION
 FLOW_ALL, FLOW_INTERIOR, FLOW_EDGES = 0, 1, 2  # tfg_ice_flow_step parts
+PREV_DEPTH = -1  # tfg_get_field / tfg_set_field index: the fp64 previous-step depth (TFG_PREV_DEPTH)
 F32, F64, I32 = 0, 1, 2
 OK, ERR_ARG, ERR_HIP, ERR_STATE, ERR_DOMAIN = 0, 1, 2, 3, 4
 

@@ -143,6 +143,35 @@ class GlacierEngine:
         self.sync()
         return out
 
+    # -- checkpoint / restart ----------------------------------------------------
+    _CKPT_STATE = ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")
+
+    def checkpoint(self, path) -> None:
+        """Save what the next step reads, so a restored engine continues bit for
+        bit: the fp64 state, the fp64 previous-step depths (TFG_PREV_DEPTH), the
+        snowfall window and the step counter (the model clock).  The
+        mass-balance integrals are not saved; they restart from zero."""
+        st = {k: self.get_field(k) for k in self._CKPT_STATE}
+        for k in ("h_snow", "h_ice"):
+            st[k] = self.get_field(k, index=nat.PREV_DEPTH)
+        st["window"] = np.stack([self.get_field("window", index=j) for j in range(self.ring_len)])
+        np.savez(path, step_index=self.step_index, ny=self.ny, nx=self.nx, **st)
+
+    def restore(self, path) -> None:
+        """Continue from a checkpoint() of a shard of the same shape.  The
+        static rasters and forcing frames are the caller's, as at the start
+        of a run; call init_state() (or fill_synthetic) first."""
+        z = np.load(path, allow_pickle=False)
+        if (int(z["ny"]), int(z["nx"])) != (self.ny, self.nx) or z["window"].shape[0] != self.ring_len:
+            raise ValueError("checkpoint of a different grid shape or snowfall-window length")
+        for k in self._CKPT_STATE:
+            self.set_field(k, z[k])
+        for k in ("h_snow", "h_ice"):
+            self.set_field(k, z[k], index=nat.PREV_DEPTH)
+        for j in range(self.ring_len):
+            self.set_field("window", z["window"][j], index=j)
+        self.step_index = int(z["step_index"])
+
     def set_inputs(self, values: np.ndarray, index: int = 0) -> None:
         """The five physics inputs of one frame in one call: values [5][n] in
         BMI order P_air, Hum_sp, P, T_air, uz (tfg_set_inputs)."""
