@@ -6,7 +6,7 @@
 // + six outputs).  Reports GB/s for several (R, W) mixes so the measured
 // k_fused rate can be placed against what this read/write mix can reach.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
-//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0] [il|pf]
+//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0] [il|pf|tb]
 // skew: extra cells between consecutive planes (plane stride = cells + skew),
 // to test whether power-of-two plane strides cost HBM channel balance.
 #include <hip/hip_runtime.h>
@@ -196,6 +196,57 @@ void run_pf(const char* name, float* in, float* out, uint32_t n, int steps, int 
   CHECK(hipEventDestroy(b));
 }
 
+
+// Time-blocked output layout: the W planes a step writes for a block of IL
+// cells sit next to that block's previous steps, i.e. out[(blk*steps + s)*W*IL
+// + w*IL + off]; reads stay planar.  A workgroup's writes over its steps then
+// fill one contiguous region instead of W planes x steps scattered regions.
+template <int R, int W, int IL>
+__global__ __launch_bounds__(256) void k_mix_tb(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
+                                                int steps, int frames) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t blk = i / IL, off = i % IL;
+    float acc = 0.0f;
+    for (int s = 0; s < steps; ++s) {
+      const float* fin = in + (size_t)(s % frames) * R * n + i;
+      float v[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[r] = fin[(size_t)r * n];
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc += v[r];
+      float* fo = out + ((size_t)blk * steps + s) * W * IL + off;
+#pragma unroll
+      for (int w = 0; w < W; ++w) __builtin_nontemporal_store(acc + (float)w, fo + (size_t)w * IL);
+    }
+  }
+}
+
+template <int R, int W, int IL>
+void run_tb(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  k_mix_tb<R, W, IL><<<g_blocks, 256>>>(in, out, n, steps, frames);  // warm-up
+  CHECK(hipGetLastError());
+  CHECK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int rep = 0; rep < 5; ++rep) {
+    CHECK(hipEventRecord(a));
+    k_mix_tb<R, W, IL><<<g_blocks, 256>>>(in, out, n, steps, frames);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    if (ms < best) best = ms;
+  }
+  const double bytes = (double)n * steps * 4.0 * (R + W);
+  std::printf("{\"mix\": \"%s\", \"read_planes\": %d, \"write_planes\": %d, \"time_block_cells\": %d, \"blocks\": %d, \"GBps\": %.1f, \"ms\": %.3f}\n",
+              name, R, W, IL, g_blocks, bytes / (best * 1e-3) / 1e9, best);
+  CHECK(hipEventDestroy(a));
+  CHECK(hipEventDestroy(b));
+}
+
 int main(int argc, char** argv) {
   const uint32_t n = argc > 1 ? (uint32_t)std::strtoul(argv[1], nullptr, 10) : 67108864u;
   const int steps = argc > 2 ? std::atoi(argv[2]) : 24;
@@ -208,6 +259,16 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(in, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
   CHECK(hipMemset(out, 0, (size_t)(n + g_skew) * 4 * 7 * frames));
+  if (argc > 5 && std::string(argv[5]) == "tb") {  // time-blocked output layout experiment only
+    run<6, 7, 1, true>("k_fused step mix, planar, nt stores", in, out, n, steps, frames);
+    run_tb<6, 7, 256>("k_fused step mix, time-blocked outputs (256 cells)", in, out, n, steps, frames);
+    run_tb<6, 7, 1024>("k_fused step mix, time-blocked outputs (1024 cells)", in, out, n, steps, frames);
+    run<6, 7, 1, true>("k_fused step mix, planar, nt stores", in, out, n, steps, frames);
+    run_tb<6, 7, 256>("k_fused step mix, time-blocked outputs (256 cells)", in, out, n, steps, frames);
+    CHECK(hipFree(in));
+    CHECK(hipFree(out));
+    return 0;
+  }
   if (argc > 5 && std::string(argv[5]) == "pf") {  // read-ahead depth experiment only
     run<6, 7, 1, true>("k_fused step mix, plain loop, nt stores", in, out, n, steps, frames);
     run_pf<6, 7, 1, 4>("k_fused step mix, read-ahead 1", in, out, n, steps, frames);
