@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
     ap.add_argument("--seed", type=int, default=20251001)
     ap.add_argument("--cpu-cells", type=int, default=1048576, help="cells in the C CPU-baseline sample")
-    ap.add_argument("--cpu-steps", type=int, default=768, help="steps of the C CPU-baseline sample (~10 s on 16 threads)")
+    ap.add_argument("--cpu-steps", type=int, default=960, help="steps of the C CPU-baseline sample (~10 s on 16 threads)")
     ap.add_argument("--parity-steps", type=int, default=96, help="steps of the GPU-vs-C-oracle spot check")
     ap.add_argument("--parity-cells", type=int, default=262144, help="cells of the GPU-vs-C-oracle spot check")
     ap.add_argument("--numpy-cells", type=int, default=393216, help="cells in the numpy (1 core) sample, 24 steps")
