@@ -210,3 +210,18 @@ def test_create_rejects_oversize_shards_before_touching_the_gpu():
     for bad in ((0, 8, nat.F32, 1, 1, 1), (8, 8, 7, 1, 1, 1), (8, 8, nat.F32, 0, 1, 1), (8, 8, nat.F32, 1, 1, 513)):
         ny, nx, eng, fr, hd, nc = bad
         assert L.tfg_create(ctypes.byref(p), ny, nx, eng, 0, fr, hd, nc, ctypes.byref(h)) == nat.ERR_ARG, bad
+
+
+def test_ice_flow_entry_points_reject_bad_arguments_without_a_device():
+    """The ice-flow ABI fails cleanly on a null handle (no HIP call is made)."""
+    import ctypes
+
+    from topoflow_glacier import _native as nat
+
+    L = nat.load()
+    out = ctypes.c_double()
+    assert L.tfg_ice_flow_step(None, 0.1, 100.0, 100.0, None, None, 0, nat.FLOW_ALL) == nat.ERR_ARG
+    assert L.tfg_ice_flow_run(None, 0.1, 100.0, 100.0, 4) == nat.ERR_ARG
+    assert L.tfg_ice_flow_dmax(None, 100.0, 100.0, None, None, 0, ctypes.byref(out)) == nat.ERR_ARG
+    assert L.tfg_ice_flow_edges(None, None, None, 0) == nat.ERR_ARG
+    assert nat.PREV_DEPTH == -1 and (nat.FLOW_ALL, nat.FLOW_INTERIOR, nat.FLOW_EDGES) == (0, 1, 2)
