@@ -40,18 +40,28 @@ ins = {"atmosphere_water__liquid_equivalent_precipitation_rate": 1e-7, "land_sur
        "atmosphere_air_water~vapor__relative_saturation": 0.003, "wind_speed_UV": 3.0}
 outs = models[0].get_output_var_names()
 buf = np.zeros(1)
+t_set = t_upd = t_get = 0.0
 t0 = time.perf_counter()
 for _ in range(steps):
     for m in models:
+        a = time.perf_counter()
         for k, v in ins.items():
             m.set_value(k, np.array([v]))
+        b = time.perf_counter()
         m.update()
+        c = time.perf_counter()
         for k in outs:
             m.get_value(k, buf)
+        d = time.perf_counter()
+        t_set += b - a
+        t_upd += c - b
+        t_get += d - c
 t_run = time.perf_counter() - t0
 ref = models[0].get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0]
 same = all(m.get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0] == ref for m in models)
 for m in models:
     m.finalize()
 print(json.dumps({"instances": n_inst, "steps": steps, "shared_stream": len(sys.argv) > 3, "create_s": t_create,
-                  "us_per_instance_step": t_run / (n_inst * steps) * 1e6, "all_instances_equal": same}))
+                  "us_per_instance_step": t_run / (n_inst * steps) * 1e6,
+                  "us_set_update_get": [round(t / (n_inst * steps) * 1e6, 2) for t in (t_set, t_upd, t_get)],
+                  "all_instances_equal": same}))
