@@ -61,7 +61,7 @@ ref = models[0].get_value("land_surface_water__runoff_volume_flux", np.zeros(1))
 same = all(m.get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0] == ref for m in models)
 for m in models:
     m.finalize()
-print(json.dumps({"instances": n_inst, "steps": steps, "shared_stream": len(sys.argv) > 3, "create_s": t_create,
+print(json.dumps({"instances": n_inst, "steps": steps, "extra_shared_stream": len(sys.argv) > 3, "create_s": t_create,
                   "us_per_instance_step": t_run / (n_inst * steps) * 1e6,
                   "us_set_update_get": [round(t / (n_inst * steps) * 1e6, 2) for t in (t_set, t_upd, t_get)],
                   "all_instances_equal": same}))

@@ -1106,6 +1106,8 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
 int tfg_destroy(tfg_handle* h) {
   if (!h) return TFG_OK;
   (void)hipSetDevice(h->device);
+  // work queued on a caller's stream (tfg_set_stream) may still use the buffers
+  if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
                   h->flow_halo, h->flow_edges, h->flow_red,

@@ -129,11 +129,29 @@ def _accessor(external: str, ctx: str):
     return property(getter, setter, doc=f"BMI variable {external}")
 
 
+_SHARED_STREAMS: dict = {}
+
+
+def _shared_stream(device: int) -> int:
+    """One HIP stream per device for every one-cell model of the process.
+    NextGen steps thousands of catchment instances in turn; one stream instead
+    of one per instance saves ~12 us per instance-step at 500 instances
+    (tests/diagnostics/bmi_many_instances.py)."""
+    if device not in _SHARED_STREAMS:
+        import torch
+
+        _SHARED_STREAMS[device] = torch.cuda.Stream(device=device)  # kept alive for the process
+    return _SHARED_STREAMS[device].cuda_stream
+
+
 def make_engine(cfg, n_frames: int = 1, hist_depth: int = 1) -> GlacierEngine:
     """The device shard a config describes (fp64 engine for one cell, fp32 for grids)."""
     engine = cfg.engine or ("float64" if cfg.ny * cfg.nx == 1 else "float32")
-    return GlacierEngine(cfg, cfg.ny, cfg.nx, engine=engine, device=cfg.device, n_frames=n_frames,
-                         hist_depth=hist_depth, fuse_steps=cfg.fuse_steps)
+    eng = GlacierEngine(cfg, cfg.ny, cfg.nx, engine=engine, device=cfg.device, n_frames=n_frames,
+                        hist_depth=hist_depth, fuse_steps=cfg.fuse_steps)
+    if cfg.ny * cfg.nx == 1:
+        eng.set_stream(_shared_stream(eng.device))
+    return eng
 
 
 def configure_engine(eng: GlacierEngine, cfg) -> bool:
