@@ -66,12 +66,16 @@ inline FlowK flow_constants(double dt, double dx, double dy, double wi, double g
   return {1.0 / dx, 1.0 / dy, 1.0 / (4.0 * dx), 1.0 / (4.0 * dy), dx / (4.0 * dt), dy / (4.0 * dt), dt / wi, gamma};
 }
 // One sub-step, LDS-tiled: a workgroup owns kFlowTX columns x kFlowRows rows
-// and walks down its strip with a three-row ring of (s, H) in LDS (one halo
-// column each side).  Each face flux is evaluated once per workgroup: the
-// row's x-faces into LDS, the y-face below each cell in a register that
-// becomes the next row's north face.  A face shared by two workgroups (or two
-// shards) is computed by both from the same values in the same order, so they
-// agree bit for bit (restatement: tests/harness.py:ice_flow_step_restated).
+// and walks down its strip with a four-row ring of (s, H) in LDS (one halo
+// column each side).  Each thread keeps its own column's values in registers
+// and reads the two neighbouring columns from LDS once per row; it evaluates
+// its west and east faces itself (the face a neighbour also evaluates comes
+// from the same values in the same order, so the two agree bit for bit) and
+// carries the south face in a register as the next row's north face.  Faces
+// shared by two workgroups (or two shards) agree the same way (restatement:
+// tests/harness.py:ice_flow_step_restated).  With four ring slots a row
+// costs one workgroup barrier: the slot written in row r (row r+2) was last
+// read in row r-1.
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS
 // accesses, not for its global loads and stores (a __syncthreads() fence would
 // drain them, and with them the rows prefetched into registers).
@@ -79,23 +83,30 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // DMAX: instead of stepping, the largest face diffusivity of the workgroup's
 // faces goes to out[workgroup] (the CFL bound of tfg_ice_flow_dmax).
-constexpr int kFlowTX = 256, kFlowRows = 32, kFlowPF = 1;  // kFlowPF rows of loads in flight (2 and 4 measured slower)
+#ifndef TFG_FLOW_ROWS
+#define TFG_FLOW_ROWS 32
+#endif
+#ifndef TFG_FLOW_WAVES
+#define TFG_FLOW_WAVES 1  // __launch_bounds__ minimum waves per SIMD
+#endif
+constexpr int kFlowTX = 256, kFlowRows = TFG_FLOW_ROWS;  // 16 and 64 rows measured no better / slower
 template <class R, bool DMAX>
-__global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
+__global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
                                                       int strip0, int strip_step, double* __restrict__ out_ice) {
 #pragma clang fp contract(off)
-  __shared__ double sS[3][kFlowTX + 2], sH[3][kFlowTX + 2], sW[3][kFlowTX + 2], qx[kFlowTX + 1];  // sW: h_iwe as read
+  __shared__ double sS[4][kFlowTX + 2], sH[4][kFlowTX + 2];  // index k = column - (c0 - 1)
+  __shared__ double red[DMAX ? kFlowTX : 1];
   double dmax = 0.0;
   const int t = threadIdx.x;
   const int64_t c0 = (int64_t)blockIdx.x * kFlowTX;
   const int64_t r0 = ((int64_t)strip0 + (int64_t)blockIdx.y * strip_step) * kFlowRows;  // this workgroup's strip
   const int64_t r1 = r0 + kFlowRows < g.ny ? r0 + kFlowRows : g.ny;
   const int64_t c = c0 + t;
-  auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) % 3; };  // 32-bit: rr - r0 + 1 <= kFlowRows + 1
-  // A row of (s, H) for columns c0-1 .. c0+kFlowTX, fetched into registers
-  // one row ahead and written to LDS a row later, so its HBM latency overlaps
-  // the current row's face arithmetic.  Raw values: (elev, h_iwe), or (s, H)
-  // from a halo row; a missing row outside the domain repeats the edge row.
+  auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) & 3; };
+  // One row, as raw values: (elev, h_iwe), or (s, H) from a halo row; a
+  // missing row outside the domain repeats the edge row.  Lane t holds its
+  // own column (j = 0); lanes 0 and 1 of wave 0 also hold the halo columns
+  // c0 - 1 and c0 + kFlowTX (j = 1, a wave-uniform branch around the loads).
   struct Raw { double a[2], b[2]; bool halo; };
   auto fetch = [&](int64_t rr, Raw& v) {
     v.halo = (rr < 0 && g.hn) || (rr >= g.ny && g.hs);
@@ -103,9 +114,8 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const Fl
     const int64_t rc_ = rr < 0 ? 0 : (rr >= g.ny ? g.ny - 1 : rr);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = t + j * kFlowTX;
-      if (k < kFlowTX + 2) {
-        const int64_t cc = c0 - 1 + k;
+      if (j == 0 || t < 64) {
+        const int64_t cc = j == 0 ? c : (t == 0 ? c0 - 1 : c0 + kFlowTX);
         const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
         if (v.halo) {
           v.a[j] = hr[cl];
@@ -117,83 +127,100 @@ __global__ __launch_bounds__(kFlowTX) void k_ice_flow(const FlowGrid g, const Fl
       }
     }
   };
-  auto put = [&](int64_t rr, const Raw& v) {
+  // own column's (s, H, h_iwe) of the rows r-1 .. r+2, rolled once per row
+  double os[4], oh[4], ow[4];
+  auto put = [&](int64_t rr, const Raw& v, int q) {
     const int sl = slot(rr);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int k = t + j * kFlowTX;
-      if (k < kFlowTX + 2) {
-        sS[sl][k] = v.halo ? v.a[j] : v.a[j] + v.b[j] * g.wi;
-        sH[sl][k] = v.halo ? v.b[j] : v.b[j] * g.wi;
-        sW[sl][k] = v.b[j];  // h_iwe of an in-domain row (the only rows a workgroup updates)
+      const double sv = v.halo ? v.a[j] : v.a[j] + v.b[j] * g.wi;
+      const double hv = v.halo ? v.b[j] : v.b[j] * g.wi;
+      if (j == 0) {
+        sS[sl][t + 1] = sv;
+        sH[sl][t + 1] = hv;
+        os[q] = sv;
+        oh[q] = hv;
+        ow[q] = v.b[j];  // h_iwe of an in-domain row (the only rows a workgroup updates)
+      } else if (t < 2) {
+        const int k = t == 0 ? 0 : kFlowTX + 1;
+        sS[sl][k] = sv;
+        sH[sl][k] = hv;
       }
     }
   };
-  auto face_y = [&](int a, int b) {  // between the rows in slots a (north) and b (south), column c
-    const double gn = (sS[b][t + 1] - sS[a][t + 1]) * K.inv_dy;
-    const double gt = ((sS[a][t + 2] - sS[a][t]) + (sS[b][t + 2] - sS[b][t])) * K.inv_4dx;
-    if constexpr (DMAX) {
-      if (c < g.nx) dmax = fmax(dmax, flow_face_D(sH[a][t + 1], sH[b][t + 1], gn, gt, K.gamma));
-      return 0.0;
-    }
-    return flow_face_q(sH[a][t + 1], sH[b][t + 1], gn, gt, K.gamma, K.lim_y);
-  };
-  // rows r0-1 and r0 first; rows r0+1 .. r0+kFlowPF in flight in registers
+  // rows r0-1 .. r0+1 into the ring, row r0+2 in flight in registers
   {
     Raw v;
     fetch(r0 - 1, v);
-    put(r0 - 1, v);
+    put(r0 - 1, v, 0);
     fetch(r0, v);
-    put(r0, v);
+    put(r0, v, 1);
+    fetch(r0 + 1, v);  // r1 >= r0 + 1
+    put(r0 + 1, v, 2);
   }
-  Raw buf[kFlowPF];
-#pragma unroll
-  for (int j = 0; j < kFlowPF; ++j)
-    if (r0 + 1 + j <= r1) fetch(r0 + 1 + j, buf[j]);
+  Raw buf;
+  if (r0 + 2 <= r1) fetch(r0 + 2, buf);
+  const bool west_ok = c >= 1 && c < g.nx, east_ok = c + 1 < g.nx;
   double qN = 0.0;
-  for (int64_t rb = r0; rb < r1; rb += kFlowPF) {
+  for (int64_t r = r0; r < r1; ++r) {
+    lds_barrier();  // rows r-1 .. r+1 are in the ring; row r-2's slot is free
+    if (r + 2 <= r1) put(r + 2, buf, 3);
+    if (r + 3 <= r1) fetch(r + 3, buf);  // in flight for the next row
+    const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
+    const double Lm = sS[rm][t], Lc = sS[rc][t], Lp = sS[rp][t], HL = sH[rc][t];
+    const double Rm = sS[rm][t + 2], Rc = sS[rc][t + 2], Rp = sS[rp][t + 2], HR = sH[rc][t + 2];
+    const double sm = os[0], sc = os[1], sp = os[2], hc = oh[1];
+    // x-faces: west (column c-1 | c) and east (c | c+1), as (left, right)
+    double qW = 0.0, qE = 0.0;
+    {
+      const double gnW = (sc - Lc) * K.inv_dx;
+      const double gtW = ((Lp - Lm) + (sp - sm)) * K.inv_4dy;
+      const double gnE = (Rc - sc) * K.inv_dx;
+      const double gtE = ((sp - sm) + (Rp - Rm)) * K.inv_4dy;
+      if constexpr (DMAX) {
+        if (west_ok) dmax = fmax(dmax, flow_face_D(HL, hc, gnW, gtW, K.gamma));
+        if (east_ok) dmax = fmax(dmax, flow_face_D(hc, HR, gnE, gtE, K.gamma));
+      } else {
+        if (west_ok) qW = flow_face_q(HL, hc, gnW, gtW, K.gamma, K.lim_x);
+        if (east_ok) qE = flow_face_q(hc, HR, gnE, gtE, K.gamma, K.lim_x);
+      }
+    }
+    // y-faces at column c: north (rows r-1 | r) on the strip's first row, then
+    // south (r | r+1), carried to the next row as its north face
+    auto face_y = [&](double sa, double sb, double ha, double hb, double La, double Ra, double Lb, double Rb) {
+      const double gn = (sb - sa) * K.inv_dy;
+      const double gt = ((Ra - La) + (Rb - Lb)) * K.inv_4dx;
+      if constexpr (DMAX) {
+        if (c < g.nx) dmax = fmax(dmax, flow_face_D(ha, hb, gn, gt, K.gamma));
+        return 0.0;
+      }
+      return flow_face_q(ha, hb, gn, gt, K.gamma, K.lim_y);
+    };
+    if (r == r0) qN = (r > 0 || g.hn) ? face_y(sm, sc, oh[0], hc, Lm, Rm, Lc, Rc) : 0.0;
+    const double qS = (r + 1 < g.ny || g.hs) ? face_y(sc, sp, hc, oh[2], Lc, Rc, Lp, Rp) : 0.0;
+    if (!DMAX && c < g.nx) {
+      const int64_t i = r * g.nx + c;
+      const double div = (qE - qW) * K.inv_dx + (qS - qN) * K.inv_dy;
+      const double v = fmax(ow[1] - K.dt_wi * div, 0.0);
+      out[i] = v;
+      if (out_ice) out_ice[i] = v * g.wi;  // writing the state plane: h_ice too (:1726)
+    }
+    qN = qS;
 #pragma unroll
-    for (int jj = 0; jj < kFlowPF; ++jj) {
-      const int64_t r = rb + jj;
-      if (r >= r1) break;
-      lds_barrier();  // row r-2's slot and qx are free
-      put(r + 1, buf[jj]);
-      if (r + 1 + kFlowPF <= r1) fetch(r + 1 + kFlowPF, buf[jj]);  // in flight for the next kFlowPF rows
-      lds_barrier();
-      const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
-      for (int k = t; k < kFlowTX + 1; k += kFlowTX) {  // x-faces between columns c0-1+k and c0+k
-        const int64_t fc = c0 - 1 + k;
-        double q = 0.0;
-        if (fc >= 0 && fc + 1 < g.nx) {
-          const double gn = (sS[rc][k + 1] - sS[rc][k]) * K.inv_dx;
-          const double gt = ((sS[rp][k] - sS[rm][k]) + (sS[rp][k + 1] - sS[rm][k + 1])) * K.inv_4dy;
-          if constexpr (DMAX) dmax = fmax(dmax, flow_face_D(sH[rc][k], sH[rc][k + 1], gn, gt, K.gamma));
-          else q = flow_face_q(sH[rc][k], sH[rc][k + 1], gn, gt, K.gamma, K.lim_x);
-        }
-        qx[k] = q;
-      }
-      if (r == r0) qN = (r > 0 || g.hn) ? face_y(rm, rc) : 0.0;
-      const double qS = (r + 1 < g.ny || g.hs) ? face_y(rc, rp) : 0.0;
-      lds_barrier();  // qx complete
-      if (!DMAX && c < g.nx) {
-        const int64_t i = r * g.nx + c;
-        const double div = (qx[t + 1] - qx[t]) * K.inv_dx + (qS - qN) * K.inv_dy;
-        const double v = fmax(sW[rc][t + 1] - K.dt_wi * div, 0.0);
-        out[i] = v;
-        if (out_ice) out_ice[i] = v * g.wi;  // writing the state plane: h_ice too (:1726)
-      }
-      qN = qS;
+    for (int q = 0; q < 3; ++q) {
+      os[q] = os[q + 1];
+      oh[q] = oh[q + 1];
+      ow[q] = ow[q + 1];
     }
   }
   if constexpr (DMAX) {
-    __syncthreads();
-    qx[t] = dmax;  // reuse qx as the reduction buffer
+    red[t] = dmax;
     __syncthreads();
     for (int w = kFlowTX / 2; w > 0; w >>= 1) {
-      if (t < w) qx[t] = fmax(qx[t], qx[t + w]);
+      if (t < w) red[t] = fmax(red[t], red[t + w]);
       __syncthreads();
     }
-    if (t == 0) out[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = qx[0];
+    if (t == 0) out[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = red[0];
   }
 }
 
