@@ -105,26 +105,27 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
   auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) & 3; };
   // One row, as raw values: (elev, h_iwe), or (s, H) from a halo row; a
   // missing row outside the domain repeats the edge row.  Lane t holds its
-  // own column (j = 0); lanes 0 and 1 of wave 0 also hold the halo columns
-  // c0 - 1 and c0 + kFlowTX (j = 1, a wave-uniform branch around the loads).
-  struct Raw { double a[2], b[2]; bool halo; };
+  // own column (j = 0); lane 0 also holds column c0 - 1 and the other lanes
+  // column c0 + kFlowTX (j = 1; put() stores those of lanes 0 and 1).
+  // (elev stays in its storage type until put(): converting at fetch time
+  // would wait for the load there and serialise the prefetch)
+  struct Raw { double a[2], b[2]; R e[2]; bool halo; };
   auto fetch = [&](int64_t rr, Raw& v) {
+    // straight-line loads (no branch, so no register merge that would wait
+    // for them): a halo row reads (s, H) from the halo; an in-domain row reads
+    // (elev, h_iwe), with the halo-s load pointed at the h_iwe row (a cache hit)
     v.halo = (rr < 0 && g.hn) || (rr >= g.ny && g.hs);
-    const double* hr = rr < 0 ? g.hn : g.hs;
     const int64_t rc_ = rr < 0 ? 0 : (rr >= g.ny ? g.ny - 1 : rr);
+    const double* hb = v.halo ? (rr < 0 ? g.hn : g.hs) + g.nx : g.iwe + rc_ * g.nx;
+    const double* ha = v.halo ? hb - g.nx : hb;
+    const R* he = static_cast<const R*>(g.elev) + rc_ * g.nx;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (j == 0 || t < 64) {
-        const int64_t cc = j == 0 ? c : (t == 0 ? c0 - 1 : c0 + kFlowTX);
-        const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
-        if (v.halo) {
-          v.a[j] = hr[cl];
-          v.b[j] = hr[g.nx + cl];
-        } else {
-          v.a[j] = (double)static_cast<const R*>(g.elev)[rc_ * g.nx + cl];
-          v.b[j] = g.iwe[rc_ * g.nx + cl];
-        }
-      }
+      const int64_t cc = j == 0 ? c : (t == 0 ? c0 - 1 : c0 + kFlowTX);
+      const int64_t cl = cc < 0 ? 0 : (cc >= g.nx ? g.nx - 1 : cc);
+      v.e[j] = he[cl];
+      v.b[j] = hb[cl];
+      v.a[j] = ha[cl];
     }
   };
   // own column's (s, H, h_iwe) of the rows r-1 .. r+2, rolled once per row
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
     const int sl = slot(rr);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const double sv = v.halo ? v.a[j] : v.a[j] + v.b[j] * g.wi;
+      const double sv = v.halo ? v.a[j] : (double)v.e[j] + v.b[j] * g.wi;
       const double hv = v.halo ? v.b[j] : v.b[j] * g.wi;
       if (j == 0) {
         sS[sl][t + 1] = sv;
