@@ -159,14 +159,14 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
     fetch(r0 + 1, v);  // r1 >= r0 + 1
     put(r0 + 1, v, 2);
   }
-  Raw buf;
-  if (r0 + 2 <= r1) fetch(r0 + 2, buf);
   const bool west_ok = c >= 1 && c < g.nx, east_ok = c + 1 < g.nx;
   double qN = 0.0;
-  for (int64_t r = r0; r < r1; ++r) {
+  // one row: `buf` holds row r+2 (fetched earlier); it is refilled with row
+  // r+ahead, in flight while this row and the next ahead-3 rows compute
+  auto row = [&](int64_t r, Raw& buf, int ahead) {
     lds_barrier();  // rows r-1 .. r+1 are in the ring; row r-2's slot is free
     if (r + 2 <= r1) put(r + 2, buf, 3);
-    if (r + 3 <= r1) fetch(r + 3, buf);  // in flight for the next row
+    if (r + ahead <= r1) fetch(r + ahead, buf);
     const int rm = slot(r - 1), rc = slot(r), rp = slot(r + 1);
     const double Lm = sS[rm][t], Lc = sS[rc][t], Lp = sS[rp][t], HL = sH[rc][t];
     const double Rm = sS[rm][t + 2], Rc = sS[rc][t + 2], Rp = sS[rp][t + 2], HR = sH[rc][t + 2];
@@ -213,7 +213,20 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
       oh[q] = oh[q + 1];
       ow[q] = ow[q + 1];
     }
+  };
+#if TFG_FLOW_PF2
+  Raw buf0, buf1;  // two rows in flight: rows of even / odd offset
+  if (r0 + 2 <= r1) fetch(r0 + 2, buf0);
+  if (r0 + 3 <= r1) fetch(r0 + 3, buf1);
+  for (int64_t r = r0; r < r1; r += 2) {
+    row(r, buf0, 4);
+    if (r + 1 < r1) row(r + 1, buf1, 4);
   }
+#else
+  Raw buf;
+  if (r0 + 2 <= r1) fetch(r0 + 2, buf);
+  for (int64_t r = r0; r < r1; ++r) row(r, buf, 3);
+#endif
   if constexpr (DMAX) {
     red[t] = dmax;
     __syncthreads();
