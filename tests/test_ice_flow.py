@@ -87,6 +87,29 @@ def test_gpu_flow_step_matches_restatement(engine):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(1, 1), (1, 300), (33, 257), (65, 513)])
+def test_gpu_flow_ragged_tiles_match_restatement(shape):
+    """Grids that leave a one-row last strip (33 = 32 + 1, 65 = 2*32 + 1) and
+    a one-column last workgroup (257, 513): the tile edges of k_ice_flow,
+    with and without halo rows, for the step and the CFL bound."""
+    g = ice_flow_gamma(BASE_CFG)
+    ny, nx = shape
+    bed, iwe = glacier_valley(ny + 2, nx)
+    b, w = bed[1:-1], iwe[1:-1]
+    north = np.stack([bed[0] + iwe[0] * WI, iwe[0] * WI])
+    south = np.stack([bed[-1] + iwe[-1] * WI, iwe[-1] * WI])
+    for halos in ((None, None), (north, south)):
+        e = _engine(b, w)
+        try:
+            assert e.ice_flow_dmax(DX, DY, *halos) == ice_flow_dmax_restated(b, w, WI, g, DX, DY, *halos)
+            e.ice_flow_step(0.001, DX, DY, *halos)
+            want = ice_flow_step_restated(b, w, WI, g, DX, DY, 0.001, *halos)
+            np.testing.assert_array_equal(e.get_field("h_iwe").reshape(w.shape), want)
+        finally:
+            e.close()
+
+
+@pytest.mark.gpu
 def test_gpu_flow_interior_then_edges_equals_whole_step():
     """TFG_FLOW_INTERIOR + TFG_FLOW_EDGES (the overlapped sharded sub-step)
     equals TFG_FLOW_ALL and the restatement bit for bit (7 row strips)."""
