@@ -37,7 +37,8 @@ e.ice_flow_run(1e-4 * reps, 100.0, 100.0, reps)  # ping-pong sub-steps, one call
 t_run = (time.perf_counter() - t0) / reps
 n = ny * nx
 # algorithmic bytes per cell and sub-step: k_ice_flow reads elev (4) + h_iwe (8),
-# writes the new h_iwe (8); k_flow_commit reads it (8), writes h_iwe and h_ice (16)
+# writes the new h_iwe (8) to scratch and h_ice (8) to the state plane;
+# k_flow_commit reads the new h_iwe (8) and writes it to the state plane (8)
 bpc = 4 + 8 + 8 + 8 + 16
 print(json.dumps({"grid": [ny, nx], "step_ms": t_step * 1e3, "run_ms_per_sub_step": t_run * 1e3, "dmax_ms": t_dmax * 1e3,
                   "cells_per_s": n / t_step, "bytes_per_cell": bpc, "GBps": n * bpc / t_step / 1e9}))

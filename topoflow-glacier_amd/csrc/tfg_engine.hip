@@ -1722,16 +1722,19 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   int first = 0, count = (int)strips, step = 1;
   if (part == TFG_FLOW_INTERIOR) { first = 1; count = (int)std::max<int64_t>(strips - 2, 0); }
   if (part == TFG_FLOW_EDGES) { count = strips > 1 ? 2 : 1; step = (int)std::max<int64_t>(strips - 1, 1); }
+  // h_ice (not read by the flow kernels) goes straight to the state plane; the
+  // new h_iwe goes to scratch, since neighbouring strips still read the old one
+  double* ice = h->st + S_HICE * h->n_pad;
   if (count > 0) {
     const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)count);
     if (h->engine == TFG_F32)
-      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, nullptr);
+      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice);
     else
-      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, nullptr);
+      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice);
     HIPCHK(h, hipGetLastError());
   }
   if (part == TFG_FLOW_INTERIOR) return TFG_OK;  // queued; the edges part commits
-  hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
+  hipLaunchKernelGGL(k_flow_commit<false>, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;
@@ -1764,7 +1767,7 @@ int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n
     HIPCHK(h, hipGetLastError());
   }
   if (n_sub & 1)
-    hipLaunchKernelGGL(k_flow_commit, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
+    hipLaunchKernelGGL(k_flow_commit<true>, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;

@@ -238,15 +238,17 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
   }
 }
 
-// commit a sub-step: the new h_iwe into the state plane, and the next step's
-// previous-step ice depth h_ice = h_iwe * wi (:1726) for the state-plane read
+// commit a sub-step: the new h_iwe into the state plane, and (ICE) the next
+// step's previous-step ice depth h_ice = h_iwe * wi (:1726) for the state-plane
+// read; without ICE the flow kernel has already written h_ice
+template <bool ICE>
 __global__ void k_flow_commit(double* __restrict__ st, const double* __restrict__ iwe_new, int64_t n, int64_t n_pad,
                               double wi) {
 #pragma clang fp contract(off)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double v = iwe_new[i];
     st[S_HIWE * n_pad + i] = v;
-    st[S_HICE * n_pad + i] = v * wi;
+    if constexpr (ICE) st[S_HICE * n_pad + i] = v * wi;
   }
 }
 
