@@ -293,8 +293,9 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
  *   TFG_FLOW_INTERIOR  the rows that read no halo row, queued asynchronously
  *                      (pass no halos); it must be followed by
  *   TFG_FLOW_EDGES     the rows next to the halos, then the commit (blocking).
- * The sub-step reads the pre-step state throughout, so ALL == INTERIOR + EDGES
- * bit for bit. */
+ * The sub-step reads the pre-step h_iwe throughout, so ALL == INTERIOR + EDGES
+ * bit for bit.  The new h_iwe lands in the state at the commit; h_ice, which
+ * the sub-step does not read, is written as each part runs. */
 enum { TFG_FLOW_ALL = 0, TFG_FLOW_INTERIOR = 1, TFG_FLOW_EDGES = 2 };
 int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
                       const double* halo_south, int halo_on_device, int part);
