@@ -162,7 +162,8 @@ int tfg_device_count(int* count);
 int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int device,
                int n_frames, int hist_depth, int n_catch, tfg_handle** out);
 
-/* Release everything.  Replaces: finalize() (:467-469). */
+/* Release everything, after the handle's stream (a caller-set one too) has
+ * drained.  Replaces: finalize() (:467-469). */
 int tfg_destroy(tfg_handle* h);
 
 /* Run the work on a caller-provided HIP stream (hipStream_t as void*), or
