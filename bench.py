@@ -12,12 +12,23 @@ no output write can be absorbed by a cache rewrite).
 Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
 HBM-resident frames, fp32 engine (fp64 state), 96 steps per launch (HBM
 footprint ~210 GB of the 288 GB: 24 forcing frames 32 GB, 96 output slots
-155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).  --gpus N: one process per GPU
-(torchrun), row-block shards of 8192 rows each (weak scaling, no data-path
-collective); value = all cells of all ranks x steps / max-over-ranks time.
+155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).
+
+--gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
+is row-partitioned over the N ranks (strong scaling, BASELINE config 4: 1024 x
+8192 per GPU at N = 8); --scaling weak gives every rank its own --ny rows.
+There is no data-path collective; value = all cells x steps / max-over-ranks
+time between barriers.
+
+The timed region is a whole number of fused launches, at least MIN_LAUNCHES,
+covering --steps; the JSON carries `steps_requested` beside the timed `steps`.
 
 Prints ONE JSON line on rank 0.  Roofline: achieved = algorithmic bytes per
-fused launch / mean launch time (HIP events on the engine's stream).
+fused launch / mean launch time (HIP events on the engine's stream); traffic
+= PMC bytes from the committed profile, only when it was measured on the same
+device code (roofline.traffic_source).  Parity spot check: GPU vs the numpy
+oracle on a sample, melt-out flips held to the fp64 baseline of the same
+sample (tests/harness.py flip_rule).
 """
 
 from __future__ import annotations
@@ -40,6 +51,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs f32
 BYTES_PER_LAUNCH = 20 + (6 * 8 + 8) * 2  # solar geometry 5xf32; state 6xf64 + window total i64, in and out
 
+MIN_LAUNCHES = 3
+
 BASE_CFG = {
     "site_prefix": "synthetic", "forcing_file": "synthetic", "dt": 1, "start_time": "2013032000",
     "end_time": "2014032000", "da": 0.0001, "slope": 50.0, "aspect": 180.0, "lon": -121.81418,
@@ -53,18 +66,20 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=480)
     ap.add_argument("--warmup", type=int, default=96)
-    ap.add_argument("--ny", type=int, default=8192, help="rows per GPU (weak) or global rows (strong)")
+    ap.add_argument("--ny", type=int, default=8192, help="global rows (strong) or rows per GPU (weak)")
     ap.add_argument("--nx", type=int, default=8192)
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--fuse", type=int, default=96, help="steps per launch (= output history slots)")
     ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
+                    help="strong (default: one --ny x --nx grid row-partitioned over the ranks, BASELINE "
+                         "config 4) or weak (--ny rows per rank)")
     ap.add_argument("--seed", type=int, default=20251001)
     ap.add_argument("--cpu-cells", type=int, default=1048576, help="cells in the C CPU-baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=960, help="steps of the C CPU-baseline sample (~10 s on 16 threads)")
-    ap.add_argument("--parity-steps", type=int, default=96, help="steps of the GPU-vs-C-oracle spot check")
-    ap.add_argument("--parity-cells", type=int, default=262144, help="cells of the GPU-vs-C-oracle spot check")
-    ap.add_argument("--numpy-cells", type=int, default=393216, help="cells in the numpy (1 core) sample, 24 steps")
+    ap.add_argument("--parity-steps", type=int, default=96, help="steps of the GPU-vs-oracle spot check")
+    ap.add_argument("--parity-cells", type=int, default=262144,
+                    help="cells of the GPU-vs-oracle spot check (also the numpy one-core sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-fed forcing) leg")
     ap.add_argument("--dt", type=float, default=1.0, help="time step [h] (BASELINE config 5: 0.25)")
@@ -96,8 +111,8 @@ def cpu_baseline(args, run_gpu_sample):
     (1) the C oracle (oracle/tfg_oracle_c.c, fp64, OpenMP over the process's CPU
         share) on --cpu-cells x --cpu-steps: the reported cpu_baseline;
     (2) the numpy oracle (oracle/tfg_oracle.py, fp64, one core) on the first
-        --numpy-cells x 24 steps, reported beside it;
-    plus a parity spot check of the GPU on the C sample's cells and steps."""
+        --parity-cells x --parity-steps, reported beside it and used as the
+        reference of a parity spot check of the GPU on those cells and steps."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import tfg_oracle as O
     import tfg_oracle_c as OC
@@ -123,35 +138,85 @@ def cpu_baseline(args, run_gpu_sample):
     cpu = {"value": n * args.cpu_steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
            "sample": f"oracle/tfg_oracle_c.c (C fp64 restatement of update(), OpenMP, {threads} threads) on the "
                      f"first {n} cells x {args.cpu_steps} hourly steps of the same synthetic workload ({t_c:.1f} s)"}
-    parity = None
+    # (2) the parity spot check and the one-core numpy leg share one numpy run:
+    # the numpy oracle (bit-identical to the reference on every golden fixture)
+    # over the first pn cells x ps steps is both the reference the GPU is checked
+    # against and the single-core CPU sample.
+    from tests.harness import flip_rule, melt_out_flips, valid_mask
+
     pn = min(args.parity_cells, n)
     ps = args.parity_steps
+    fnp = {k: v[frames[:ps], :pn] for k, v in forcing.items()}
+    snp = {k: v[:pn] for k, v in static.items()}
+    t0 = time.perf_counter()
+    ref, _ = O.run_oracle(cfg, snp, fnp, ps, clock=(clock[0], clock[3]))
+    t_np = time.perf_counter() - t0
+    numpy_leg = {"value": pn * ps / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+                 "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on the first {pn} cells x "
+                           f"{ps} steps ({t_np:.1f} s)"}
+    parity = None
     gpu = run_gpu_sample(pn, ps)
     if gpu is not None:
-        # every step of the first pn cells, GPU history vs the C oracle; cells whose
-        # trajectories part at a melt-out residual (DESIGN.md "Melt-out flips") are
-        # compared up to the flip and counted
-        from tests.harness import melt_out_flips, valid_mask
-
-        ref, _ = OC.run_oracle_c(cfg, {k: v[:pn] for k, v in static.items()},
-                                 {k: np.ascontiguousarray(v[:, :pn]) for k, v in forcing.items()}, ps,
+        # Every step of the first pn cells.  Cells whose trajectories part at a
+        # melt-out residual (DESIGN.md "Melt-out flips") are compared up to the
+        # flip and counted; the count is held to the fp64 baseline of the same
+        # cells and steps: the C oracle against the numpy oracle, two fp64
+        # restatements that differ only in their libm (tests/harness.py flip_rule).
+        names = sorted(gpu)
+        ref = {k: ref[k] for k in names}
+        c64, _ = OC.run_oracle_c(cfg, snp, {k: np.ascontiguousarray(v[:, :pn]) for k, v in forcing.items()}, ps,
                                  clock=(clock[0][:ps], clock[3][:ps]), frames=frames[:ps], hist=True, nthreads=threads)
+        flip64, genuine64 = melt_out_flips({k: c64[k] for k in names}, ref)
         flip, genuine = melt_out_flips(gpu, ref)
         ok = valid_mask(flip, ps)
-        parity = {"vs": "C oracle", "cells": pn, "steps": ps, "outputs": sorted(gpu),
-                  "max_floored_rel": max(_floored_rel(g[ok], ref[k][ok])[0] for k, g in gpu.items()),
-                  "tolerance": 1e-5, "melt_out_flips": int((flip >= 0).sum()), "genuine_mismatches": len(genuine)}
-    # (2) numpy oracle, one core
-    m = min(args.numpy_cells, n)
-    fnp = {k: syn[k][frames[:24], :m].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
-    snp = {k: v[:m] for k, v in static.items()}
-    t0 = time.perf_counter()
-    O.run_oracle(cfg, snp, fnp, min(24, steps), clock=(clock[0], clock[3]))
-    t_np = time.perf_counter() - t0
-    numpy_leg = {"value": m * min(24, steps) / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-                 "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on the first {m} cells x "
-                           f"{min(24, steps)} hourly steps ({t_np:.1f} s)"}
+        err = max(_floored_rel(g[ok], ref[k][ok])[0] for k, g in gpu.items())
+        rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
+        parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "cells": pn, "steps": ps,
+                  "outputs": names, "max_floored_rel": err, "tolerance": 1e-5,
+                  "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"],
+                  "flip_ratio": rule["ratio"], "flip_budget": rule["budget"], "flip_rule": rule["rule"],
+                  "genuine_mismatches": len(genuine), "fp64_baseline_genuine_mismatches": len(genuine64),
+                  "ok": bool(err <= 1e-5 and not genuine and rule["ok"])}
     return cpu, numpy_leg, parity
+
+
+def shard_plan(args, world: int, rank: int) -> dict:
+    """This rank's rows.  The default is strong scaling: the ONE --ny x --nx
+    grid of BASELINE config 4 row-partitioned over the ranks (the whole grid at
+    N = 1, 1024 x 8192 per GPU at N = 8); --scaling weak gives each rank --ny
+    rows of a taller grid."""
+    from topoflow_glacier.sharding import row_block
+
+    scaling = args.scaling or "strong"  # the same label at every N of the driver's SCALE series
+    if scaling == "weak":
+        ny_global, row0, rows = args.ny * world, rank * args.ny, args.ny
+    else:
+        ny_global = args.ny
+        row0, rows = row_block(args.ny, rank, world)
+    rows_max = max(row_block(ny_global, r, world)[1] for r in range(world)) if scaling == "strong" else rows
+    return {"scaling": scaling, "ny_global": ny_global, "row0": row0, "rows": rows,
+            "workload": f"{ny_global}x{args.nx} grid ({rows_max}x{args.nx} per GPU)"}
+
+
+def pmc_traffic(rows, args):
+    """HBM bytes per launch from the committed PMC profile of this shard shape
+    (scripts/gpu_pmc.sh -> profiles/pmc_<nx>x<rows>_fuse<K>.json), quoted only
+    when the profile was measured on device code identical to the running
+    library's (sha256 of its .hip_fatbin section); otherwise null, with the reason."""
+    from topoflow_glacier import _native as nat
+
+    pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}.json"
+    running = nat.code_object_sha256()
+    if args.engine != "float32" or args.catchments or args.dt != 1.0:
+        return None, {"profile": None, "reason": "no PMC profile for this variant of the kernel"}
+    if not pmc.exists():
+        return None, {"profile": None, "reason": f"{pmc.relative_to(ROOT)} not measured"}
+    prof = json.loads(pmc.read_text())
+    measured = prof.get("code_object_sha256")
+    src = {"profile": str(pmc.relative_to(ROOT)), "code_object_sha256": measured,
+           "running_code_object_sha256": running, "match": measured is not None and measured == running,
+           "read_scale": (prof.get("correction") or {}).get("read_scale")}
+    return (prof.get("hbm_bytes_per_launch") if src["match"] else None), src
 
 
 def catchment_blocks(row0, rows, ny_global, nx, k):
@@ -197,7 +262,7 @@ def main():
 
     from topoflow_glacier.bmi.config import TopoflowGlacierConfig
     from topoflow_glacier.engine import GlacierEngine
-    from topoflow_glacier.sharding import allreduce_diagnostics, row_block
+    from topoflow_glacier.sharding import allreduce_diagnostics
     from topoflow_glacier.synthetic import diurnal_table
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -214,12 +279,9 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    if args.scaling == "weak":
-        ny_global = args.ny * world
-        row0, rows = rank * args.ny, args.ny
-    else:
-        ny_global = args.ny
-        row0, rows = row_block(args.ny, rank, world)
+    plan = shard_plan(args, world, rank)
+    args.scaling = plan["scaling"]
+    ny_global, row0, rows = plan["ny_global"], plan["row0"], plan["rows"]
     cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
     n_catch = args.catchments + 1 if args.catchments > 0 else 1
     eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
@@ -239,7 +301,10 @@ def main():
     # warmup (untimed)
     eng.run(args.warmup)
     barrier()
-    n_launch = max(1, args.steps // args.fuse)
+    # Whole fused launches, and at least MIN_LAUNCHES of them, so that a short
+    # --steps still gives a multi-launch timed region; the JSON carries the
+    # requested count beside the timed one.
+    n_launch = max(MIN_LAUNCHES, -(-args.steps // args.fuse))
     steps = n_launch * args.fuse
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
     barrier()
@@ -286,16 +351,20 @@ def main():
                     se.close()
 
             cpu, numpy_leg, parity = cpu_baseline(args, run_gpu_sample)
-        traffic = None
-        pmc = ROOT / "profiles" / f"pmc_{args.nx}x{args.ny}_fuse{args.fuse}.json"
-        if pmc.exists():
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        traffic, traffic_source = pmc_traffic(rows, args)
         result = {
             "metric": METRIC,
             "value": value,
             "unit": "cell-updates/s",
             "n_gpus": world,
             "steps": steps,
+            "steps_requested": args.steps,
+            "steps_note": None if steps == args.steps else (
+                f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps, at least {MIN_LAUNCHES} "
+                f"launches) to cover the {args.steps} requested: a launch keeps each cell's state in registers "
+                f"across its {args.fuse} steps, so the timed region is a whole number of launches"),
+            "launches": {"count": n_launch, "steps_each": args.fuse, "ms_min": float(launch_ms.min()),
+                         "ms_mean": float(launch_ms.mean()), "ms_max": float(launch_ms.max())},
             "warmup": args.warmup,
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
@@ -304,7 +373,7 @@ def main():
             "dtype": "f32" if args.engine == "float32" else "f64",
             "data": "synthetic (counter-hash DEM/forcing with CSV statistics, 24 HBM-resident hourly frames)",
             "config": {
-                "workload": f"{ny_global}x{args.nx} grid ({rows}x{args.nx} per GPU), {args.dt:g} h steps, "
+                "workload": f"{plan['workload']}, {args.dt:g} h steps, "
                             f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch"
                             + (f", {args.catchments} catchments" if args.catchments else ""),
                 "grid_per_gpu": [rows, args.nx],
@@ -319,6 +388,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
                 "kernel_ms_per_launch": float(launch_ms.mean()),
             },

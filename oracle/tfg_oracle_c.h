@@ -37,6 +37,17 @@ int orc_run(const orc_params* c, int64_t ncell, int nsteps, const double* elev, 
             const double* h0_iwe, const double* const* forcing, const int32_t* frame, const double* jd,
             const double* tsn, double* out_last, double* out_hist, double* diag, int nthreads);
 
+/* orc_run from a mid-run state instead of the initialize() state (:274-411):
+ *   state0: [8][ncell] h_snow, h_ice (previous-step depths), h_swe, h_iwe, Eccs,
+ *     Ecci, albedo, n; or NULL for the initial state from h0_*
+ *   ring0: [ncell][ring_len] snowfall window, oldest slot first (the numpy
+ *     oracle's `ring` attribute); or NULL for an empty window */
+int orc_run_from(const orc_params* c, int64_t ncell, int nsteps, const double* elev, const double* slope,
+                 const double* aspect, const double* h0_snow, const double* h0_ice, const double* h0_swe,
+                 const double* h0_iwe, const double* state0, const double* ring0, const double* const* forcing,
+                 const int32_t* frame, const double* jd, const double* tsn, double* out_last, double* out_hist,
+                 double* diag, int nthreads);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

@@ -1,9 +1,12 @@
-# PMC passes on the bench workload (counters in separate passes; no tracing domains).
+# PMC passes on the bench workload (one counter set per pass; no tracing domains),
+# then the 4-byte-lane calibration passes on tools/hbm_mix, then the profile JSON
+# bench.py quotes (scripts/pmc_profile.py; PMC_PROFILE names it).
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${PMC_TAG:-pmc}
 mkdir -p $OUT
-ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --steps 48 --warmup 24 --no-cpu-baseline --no-pcie}"
+# every k_fused dispatch of this run is a full 96-step launch (warm-up included)
+ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --steps 96 --warmup 96 --no-cpu-baseline --no-pcie}"
 i=0
 while IFS= read -r line; do
   [ -z "$line" ] && continue
@@ -11,12 +14,15 @@ while IFS= read -r line; do
   timeout -k 10 300 rocprofv3 --pmc $line --output-format csv -d $OUT/p$i -o run -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($line) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
-done <<'PASSES'
+done <<PASSES
 FETCH_SIZE
 WRITE_SIZE
-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY
-GRBM_GUI_ACTIVE SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR
-SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_SMEM SQ_INSTS_BRANCH
-TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum
+${PMC_EXTRA:-}
 PASSES
-find $OUT -name "*counter_collection*.csv" | head
+for c in FETCH_SIZE WRITE_SIZE; do
+  d=$OUT/cal_$(echo $c | cut -d_ -f1 | tr A-Z a-z)
+  timeout -k 10 120 rocprofv3 --pmc $c --output-format csv -d $d -o run -- tools/hbm_mix 67108864 8 2048 0 cal > $d.log 2>&1
+  rc=$?; echo "calibration $c rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
+done
+python3 scripts/pmc_profile.py $OUT ${PMC_PROFILE:-$OUT/profile.json} 8192 8192 96 67108864 8

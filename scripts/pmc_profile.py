@@ -1,0 +1,109 @@
+"""Turn the rocprofv3 --pmc passes of scripts/gpu_pmc.sh into the traffic
+profile bench.py quotes (profiles/pmc_<nx>x<ny>_fuse<K>.json).
+
+  python3 scripts/pmc_profile.py <pmc dir> <out json> [nx ny fuse]
+
+* k_fused passes: <dir>/p*/run_counter_collection.csv (one counter set each).
+* Calibration passes: <dir>/cal_fetch, <dir>/cal_write (tools/hbm_mix ... cal):
+  streaming kernels with known bytes per dispatch give the FETCH_SIZE and
+  WRITE_SIZE scale for 4-byte lanes, the width k_fused uses.  The guide's
+  gfx950 FETCH_SIZE x2 is calibrated for 16-byte lanes only
+  (MI355X_MICROARCH.md, HBM/rocprofv3 section); this file records both.
+* code_object_sha256: the sha256 of the measured library's .hip_fatbin
+  section.  bench.py quotes `traffic` only when the running library's device
+  code has the same hash.
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "topoflow-glacier_amd"))
+from topoflow_glacier._native import code_object_sha256  # noqa: E402
+
+BYTES_PER_STEP, BYTES_PER_LAUNCH = 52, 132  # bench.py / DESIGN.md section 5
+
+
+def per_dispatch(paths, match):
+    """{counter: mean value per dispatch} over kernels whose name contains `match`."""
+    vals = defaultdict(list)
+    for f in paths:
+        per = defaultdict(lambda: defaultdict(float))
+        for row in csv.DictReader(open(f)):
+            if match not in row["Kernel_Name"]:
+                continue
+            per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+        for c, d in per.items():
+            vals[c] += [d[k] for k in sorted(d, key=int)]
+    return {c: sum(v) / len(v) for c, v in vals.items() if v}
+
+
+def calibration(d: Path, cells: int, steps: int):
+    """Counter KiB x 1024 / known bytes for each calibration kernel (first
+    dispatch is the warm-up; all dispatches move the same bytes)."""
+    kernels = {  # tools/hbm_mix.hip k_mix<R, W, V, NT>
+        "read only 4 B/lane": ("k_mix<7, 0, 1, false>", "FETCH_SIZE", 7),
+        "read only 16 B/lane": ("k_mix<7, 0, 4, false>", "FETCH_SIZE", 7),
+        "write only 4 B/lane": ("k_mix<0, 7, 1, false>", "WRITE_SIZE", 7),
+        "write only 4 B/lane nt": ("k_mix<0, 7, 1, true>", "WRITE_SIZE", 7),
+        "k_fused mix reads 4 B/lane nt": ("k_mix<6, 7, 1, true>", "FETCH_SIZE", 6),
+        "k_fused mix writes 4 B/lane nt": ("k_mix<6, 7, 1, true>", "WRITE_SIZE", 7),
+    }
+    out = {}
+    for name, (kern, counter, planes) in kernels.items():
+        sub = "cal_fetch" if counter == "FETCH_SIZE" else "cal_write"
+        v = per_dispatch(glob.glob(str(d / sub / "run_counter_collection.csv")), kern).get(counter)
+        if v is None:
+            continue
+        known = cells * steps * 4 * planes
+        out[name] = {"counter": counter, "counter_bytes": v * 1024, "known_bytes": known,
+                     "counter_over_known": v * 1024 / known}
+    return out
+
+
+def main():
+    d, out = Path(sys.argv[1]), Path(sys.argv[2])
+    nx, ny, fuse = (int(x) for x in sys.argv[3:6]) if len(sys.argv) > 5 else (8192, 8192, 96)
+    raw = per_dispatch(sorted(glob.glob(str(d / "p*" / "run_counter_collection.csv"))), "k_fused<float, false, false")
+    cal = calibration(d, cells=int(sys.argv[6]) if len(sys.argv) > 6 else 67108864,
+                      steps=int(sys.argv[7]) if len(sys.argv) > 7 else 8)
+    rd_scale = 1.0 / cal["read only 4 B/lane"]["counter_over_known"] if "read only 4 B/lane" in cal else 2.0
+    wr_scale = 1.0 / cal["write only 4 B/lane nt"]["counter_over_known"] if "write only 4 B/lane nt" in cal else 1.0
+    rd = raw["FETCH_SIZE"] * 1024 * rd_scale
+    wr = raw["WRITE_SIZE"] * 1024 * wr_scale
+    alg = nx * ny * (BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH)
+    res = {
+        "kernel": f"k_fused<float,false,false,false,1> (fp32 engine, {fuse} steps fused) at {nx}x{ny}",
+        "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "
+                   "calibration: rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE -- tools/hbm_mix 67108864 8 2048 0 cal); "
+                   "python3 scripts/pmc_profile.py",
+        "code_object_sha256": code_object_sha256(),
+        "correction": {
+            "read_scale": rd_scale, "write_scale": wr_scale,
+            "source": "measured on this box: tools/hbm_mix cal kernels with known bytes, 4 B lanes (k_fused's width); "
+                      "the guide's x2 FETCH_SIZE correction is calibrated for 16 B lanes",
+            "calibration": cal,
+        },
+        "hbm_read_bytes_per_launch": rd,
+        "hbm_write_bytes_per_launch": wr,
+        "hbm_bytes_per_launch": rd + wr,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (rd + wr) / alg,
+        "raw_counters_mean_per_dispatch": raw,
+    }
+    waves = raw.get("SQ_WAVES")
+    if waves:
+        cells_per_lane = nx * ny / (waves * 64)
+        res["per_wave_step"] = {k: v / (waves * fuse * cells_per_lane) for k, v in raw.items()
+                                if k.startswith("SQ_") and k != "SQ_WAVES"}
+    out.write_text(json.dumps(res, indent=1) + "\n")
+    print(json.dumps({k: res[k] for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch",
+                                          "traffic_over_algorithmic", "code_object_sha256")}))
+    print(json.dumps(cal, indent=1))
+
+
+if __name__ == "__main__":
+    main()

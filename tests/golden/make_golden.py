@@ -27,9 +27,12 @@ Fixtures written (all small .npz, float64):
 * ``satterlund.npz`` -- SATTERLUND = True (the alternative vapour-pressure and
   emissivity formulas).
 * ``params.npz`` -- non-default dust_atten / canopy_factor / cloud_factor.
+* ``clock_phoenix.npz``, ``clock_anchorage.npz`` -- runs outside
+  America/Los_Angeles across a DST change (central Arizona, no DST; Wolverine
+  Glacier, Alaska), carrying the zone name the timezonefinder stub returned.
 
 Usage:  python3 tests/golden/make_golden.py   (takes ~1 minute)
-        python3 tests/golden/make_golden.py --only satterlund,params
+        python3 tests/golden/make_golden.py --only satterlund,params,zones
 """
 
 from __future__ import annotations
@@ -56,11 +59,20 @@ SHIMS = {
         class Bmi:
             pass
     """,
+    # timezonefinder's polygon data is not available offline.  The stub answers
+    # what its polygons give for the points the fixtures use: the Pacific
+    # Northwest box (every reference config), central Arizona (34.0 N,
+    # 111.5 W: America/Phoenix, no DST) and Wolverine Glacier, Alaska
+    # (60.4 N, 148.9 W: America/Anchorage).
     "timezonefinder.py": """
         class TimezoneFinder:
             def timezone_at(self, lat=None, lng=None):
                 if -125 <= lng <= -114 and 32 <= lat <= 49.5:
                     return "America/Los_Angeles"
+                if abs(lat - 34.0) < 0.01 and abs(lng + 111.5) < 0.01:
+                    return "America/Phoenix"
+                if abs(lat - 60.4) < 0.01 and abs(lng + 148.9) < 0.01:
+                    return "America/Anchorage"
                 return None
             def certain_timezone_at(self, lat=None, lng=None):
                 return self.timezone_at(lat=lat, lng=lng)
@@ -298,6 +310,25 @@ def build_clock_windows():
     return parts
 
 
+ZONE_WINDOWS = (  # (tag, lat, lon, zone the stub returns, start, steps): each crosses a US DST change
+    ("phoenix", 34.0, -111.5, "America/Phoenix", "2014030712", 96),
+    ("anchorage", 60.4, -148.9, "America/Anchorage", "2013110112", 96),
+)
+
+
+def build_zone_windows():
+    """Runs outside America/Los_Angeles, so the reference's own
+    gmt_offset_hours (solar_funcs.py:1616-1637) and zoneinfo pin the UTC
+    offset of another zone: Arizona keeps -7 across the DST start, Alaska
+    goes from -8 to -9 at the DST end."""
+    parts = []
+    for tag, lat, lon, zone, start, n in ZONE_WINDOWS:
+        cells, forc = _perturbed_cells(4, n, 13, start, extra_cfg={"lat": lat, "lon": lon})
+        r = _run_job({"nsteps": n, "cells": cells})
+        parts.append((tag, zone, forc, r, [c["cfg"] for c in cells]))
+    return parts
+
+
 def build_dt(dt, float_dt, nsteps, ncell=8):
     cells, forc = _perturbed_cells(ncell, nsteps, 99, "2013032000", extra_cfg={"dt": dt})
     r = _run_job({"nsteps": nsteps, "cells": cells, "float_dt": float_dt})
@@ -344,6 +375,9 @@ def main(only=None):
         if "params" in only:
             f, r, c = build_variant({"dust_atten": 0.14, "canopy_factor": 0.2, "cloud_factor": 0.45}, seed=32)
             _save("params.npz", f, r, c)
+        if "zones" in only:
+            for tag, zone, f, r, c in build_zone_windows():
+                _save(f"clock_{tag}.npz", f, r, c, tz_name=zone)
         return
     f, r, c = build_cat3062920()
     _save("cat3062920_265.npz", f, r, c)
@@ -355,6 +389,7 @@ def main(only=None):
     _save("dt2.npz", f, r, c)
     f, r, c = build_dt(0.25, True, 400)
     _save("dt_quarter.npz", f, r, c)
+    main(["satterlund", "params", "zones"])
 
 
 if __name__ == "__main__":

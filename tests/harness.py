@@ -47,6 +47,8 @@ def load_golden(name: str) -> dict:
         "internal": {n: z["internal"][j] for j, n in enumerate(z["internal_names"])},
         "nsteps": F.shape[1],
         "ncell": F.shape[2],
+        # the zone the reference's timezonefinder stub returned (make_golden.py)
+        "tz_name": str(z["tz_name"]) if "tz_name" in z.files else "America/Los_Angeles",
     }
 
 
@@ -57,10 +59,12 @@ def cfg_object(cfg: dict):
     return TopoflowGlacierConfig.model_validate(cfg)
 
 
-def oracle_run(cfg: dict, static: dict, forcing: dict, nsteps: int | None = None, catch_id=None):
+def oracle_run(cfg: dict, static: dict, forcing: dict, nsteps: int | None = None, catch_id=None,
+               tz_name: str = "America/Los_Angeles"):
     out, m = O.run_oracle(cfg, {"elev": static["elev"], "slope": static["slope"], "aspect": static["aspect"],
                                 "h0_snow": static["h0_snow"], "h0_ice": static["h0_ice"],
-                                "h0_swe": static["h0_swe"], "h0_iwe": static["h0_iwe"]}, forcing, nsteps)
+                                "h0_swe": static["h0_swe"], "h0_iwe": static["h0_iwe"]}, forcing, nsteps,
+                          tz_name=tz_name)
     return out, m
 
 
@@ -145,6 +149,55 @@ def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
             genuine.append((int(c), k, [v for v in names if np.abs(np.asarray(gpu[v])[k, c] - np.asarray(ref[v])[k, c])
                                         > rtol * max(abs(np.asarray(ref[v])[k, c]), scale_floor(ref[v]))]))
     return flip, genuine
+
+
+# One flip budget for every parity check (tests, smoke, bench).  The melt-out
+# gates test fp64 state for exact zero, so ANY two implementations that differ in
+# the last bit flip some cells.  The yardstick is the fp64 baseline of the same
+# cells and steps: the C oracle (glibc libm) against the numpy oracle (numpy's
+# SIMD libm, bit-exact to the reference fixtures) -- two fp64 restatements of
+# the same operation order.  Measured ratio GPU fp32 / fp64 baseline: 1.93 on
+# bench.py's sample (4157 / 2149 of 262 144 cells x 96 steps) and 1.9 on the
+# year-long run (ice divergence 3.5 % / 1.8 % of 2048 cells); DESIGN.md section 3.
+FLIP_RATIO_MAX = 3.0
+FLIP_SLACK = 3  # absolute allowance for samples whose baseline is a handful of cells
+
+
+def flip_rule(flips: int, fp64_flips: int) -> dict:
+    """The one budget: flips <= FLIP_RATIO_MAX x fp64 baseline flips + FLIP_SLACK."""
+    budget = int(FLIP_RATIO_MAX * fp64_flips) + FLIP_SLACK
+    return {"flips": int(flips), "fp64_flips": int(fp64_flips), "budget": budget,
+            "ratio": (flips / fp64_flips) if fp64_flips else None, "ok": bool(flips <= budget),
+            "rule": f"flips <= {FLIP_RATIO_MAX:g} x fp64 baseline (C oracle vs numpy oracle, same cells and steps)"
+                    f" + {FLIP_SLACK}"}
+
+
+def c_oracle_hist(cfg: dict, static: dict, forcing: dict, nsteps: int, frames=None, state=None, clock=None,
+                  start_step: int = 0, tz_name: str = "America/Los_Angeles"):
+    """The C oracle (fp64, glibc libm) over the same cells and steps as a numpy
+    oracle run: per-step outputs [nsteps][ncell].  `forcing` is [n_frames][ncell]
+    per field and step k reads frames[k] (default k); `state` starts it from a
+    numpy-oracle snapshot; `clock` = (jd, tsn) arrays of at least start_step+nsteps."""
+    import tfg_oracle_c as OC
+
+    if clock is None:
+        jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], start_step + nsteps, cfg["lon"], tz_name)
+    else:
+        jd, tsn = clock
+    jd = np.asarray(jd)[start_step:start_step + nsteps]
+    tsn = np.asarray(tsn)[start_step:start_step + nsteps]
+    st = {k: np.asarray(static[k], np.float64) for k in STATIC_KEYS}
+    f = {k: np.ascontiguousarray(np.asarray(v, np.float64)) for k, v in forcing.items()}
+    out, _ = OC.run_oracle_c(cfg, st, f, nsteps, clock=(jd, tsn), frames=frames, hist=True, state=state)
+    return out
+
+
+def fp64_baseline_flips(c_out: dict, ref: dict, rtol: float = 1e-5) -> int:
+    """Melt-out flips of the C oracle against the numpy oracle (or the reference)."""
+    names = [v for v in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") if v in ref]
+    flip, genuine = melt_out_flips({v: c_out[v] for v in names}, {v: ref[v] for v in names}, rtol)
+    assert not genuine, f"C oracle vs numpy oracle: {genuine[:5]}"
+    return int((flip >= 0).sum())
 
 
 def valid_mask(flip: np.ndarray, nsteps: int) -> np.ndarray:
@@ -245,6 +298,10 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     finally:
         eng.close()
     ref, m = oracle_synthetic(seed, ny, nx, nsteps, n_frames, cfg_over=cfg_over)
+    static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"], "h0_snow": syn["h_snow"],
+              "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
+    c64 = c_oracle_hist(cfg, static, {k: syn[k] for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}, nsteps,
+                        frames=np.arange(nsteps) % n_frames)
     report = {}
     worst = 0.0
     worst_rel = 0.0
@@ -268,12 +325,14 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     report["diag"] = (float(np.max(drel[[0, 1, 2, 5]])), 0.0)
     worst_rel = max(worst, report["diag"][0])
     n_flip = int((flip >= 0).sum())
-    ok = worst_rel <= tol and not genuine and n_flip <= max(1, int(0.01 * flip.size))
-    summary = ", ".join(f"{k}={v[0]:.2e}" for k, v in report.items()) + f", melt-out flips={n_flip}/{flip.size}"
+    rule = flip_rule(n_flip, fp64_baseline_flips(c64, ref, tol))
+    ok = worst_rel <= tol and not genuine and rule["ok"]
+    summary = (", ".join(f"{k}={v[0]:.2e}" for k, v in report.items())
+               + f", melt-out flips={n_flip}/{flip.size} (fp64 baseline {rule['fp64_flips']}, budget {rule['budget']})")
     if genuine:
         summary += f", FAILURES={genuine[:5]}"
     return {"ok": ok, "max_rel": worst_rel, "report": report, "summary": summary, "gpu": gpu, "ref": ref,
-            "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine}
+            "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine, "flip_rule": rule}
 
 
 def terrain_dem(ny: int, nx: int) -> np.ndarray:

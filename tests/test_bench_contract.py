@@ -1,21 +1,53 @@
 """bench.py keeps the driver's contract: one JSON line on stdout with the
-metric, value, roofline and cpu_baseline objects (small workload)."""
+metric, value, roofline and cpu_baseline objects (small workload, GPU), and
+its shard plan partitions BASELINE config 4's one grid over N ranks (CPU)."""
 
 import json
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 from tests.harness import ROOT
 
-pytestmark = pytest.mark.gpu
+
+def _args(*argv):
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    old = sys.argv
+    try:
+        sys.argv = ["bench.py", *argv]
+        return bench, bench.parse()
+    finally:
+        sys.argv = old
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_default_shard_plan_is_config4_strong_scaling(world):
+    """--gpus N (the driver's SCALE runs) splits ONE 8192 x 8192 grid by rows:
+    every row exactly once, 8192 / N rows per rank; N = 1 is the whole grid."""
+    bench, args = _args("--gpus", str(world))
+    plans = [bench.shard_plan(args, world, r) for r in range(world)]
+    assert all(p["ny_global"] == 8192 for p in plans)
+    rows = np.concatenate([np.arange(p["row0"], p["row0"] + p["rows"]) for p in plans])
+    assert np.array_equal(rows, np.arange(8192))
+    assert plans[0]["workload"] == f"8192x8192 grid ({8192 // world}x8192 per GPU)"
+    assert plans[0]["scaling"] == "strong"  # one label for the driver's whole N = 1, 2, 4, 8 series
+
+
+def test_weak_scaling_stays_behind_its_flag():
+    bench, args = _args("--gpus", "4", "--scaling", "weak")
+    p = [bench.shard_plan(args, 4, r) for r in range(4)]
+    assert p[3]["row0"] == 3 * 8192 and p[3]["rows"] == 8192 and p[0]["workload"] == "32768x8192 grid (8192x8192 per GPU)"
+
+
+@pytest.mark.gpu
 def test_bench_prints_one_json_line_with_the_contract_keys():
     cmd = [sys.executable, str(ROOT / "bench.py"), "--ny", "256", "--nx", "1024", "--steps", "48", "--warmup", "24",
            "--fuse", "24", "--cpu-cells", "4096", "--cpu-steps", "48", "--parity-cells", "2048", "--parity-steps", "24",
-           "--numpy-cells", "1024", "--no-pcie"]
+           "--no-pcie"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -24,8 +56,11 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    assert d["n_gpus"] == 1 and d["steps"] == 48 and d["value"] > 0 and d["higher_is_better"] is True
-    assert d["config"]["workload"] and d["dtype"] == "f32" and d["scaling"] == "weak"
+    # --steps 48 with 24-step launches: at least 3 whole launches are timed
+    assert d["n_gpus"] == 1 and d["steps"] == 72 and d["steps_requested"] == 48 and d["steps_note"]
+    assert d["launches"]["count"] == 3 and d["launches"]["ms_min"] <= d["launches"]["ms_mean"] <= d["launches"]["ms_max"]
+    assert d["value"] > 0 and d["higher_is_better"] is True
+    assert d["config"]["workload"] and d["dtype"] == "f32" and d["scaling"] == "strong"
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
@@ -33,3 +68,6 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] in ("port", "reference") and cb["sample"]
     sp = d["sample_parity"]
     assert sp["genuine_mismatches"] == 0 and sp["max_floored_rel"] <= sp["tolerance"]
+    assert sp["ok"] and sp["melt_out_flips"] <= sp["flip_budget"] and "flips_fp64_baseline" in sp
+    ts = rf["traffic_source"]  # no PMC profile of this shape: traffic is null and says why
+    assert rf["traffic"] is None and ts["reason"]

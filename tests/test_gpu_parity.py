@@ -10,7 +10,10 @@ Tolerances
                 the variable's non-zero values.
   Melt-out residual flips (tests/harness.py:melt_out_flips) are the one
   discontinuity a last-bit state difference can toggle; a flipped cell is
-  compared up to its flip step, and flips must stay rare.
+  compared up to its flip step.  Every test holds the flip count to ONE rule
+  (tests/harness.py:flip_rule): at most FLIP_RATIO_MAX x the flips of the fp64
+  baseline on the same cells and steps (the C oracle against the numpy oracle
+  or the reference fixture) + FLIP_SLACK.
 """
 
 import numpy as np
@@ -18,8 +21,9 @@ import pandas as pd
 import pytest
 import yaml
 
-from tests.harness import (BASE_CFG, GOLDEN, OUT_NAMES, gpu_run_fields, load_golden, make_engine, melt_out_flips,
-                           oracle_run, parity, run_gpu_vs_oracle, synthetic_inputs, valid_mask)
+from tests.harness import (BASE_CFG, GOLDEN, OUT_NAMES, c_oracle_hist, flip_rule, fp64_baseline_flips, gpu_run_fields,
+                           load_golden, make_engine, melt_out_flips, oracle_run, parity, run_gpu_vs_oracle,
+                           synthetic_inputs, valid_mask)
 
 pytestmark = pytest.mark.gpu
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
@@ -153,14 +157,16 @@ def test_update_until_equals_repeated_update(tmp_path):
 
 # ---------------------------------------------------------------- engines vs reference fixtures
 @pytest.mark.parametrize("name", ["grid64", "dt2", "dt_quarter", "clock_dst_end", "clock_dst_start", "clock_new_year",
-                                  "satterlund", "params"])
+                                  "satterlund", "params", "clock_phoenix", "clock_anchorage"])
 def test_fp64_engine_vs_reference_fixtures(name):
     g = load_golden(name)
     n = g["ncell"]
     outs, state, diag = gpu_run_fields(g["cfg"], g["static"], g["forcing"], 1, n, "float64", g["nsteps"])
     flip, genuine = melt_out_flips(outs, g["outputs"], 1e-10)
     assert not genuine, genuine
-    assert (flip >= 0).sum() <= max(1, n // 32), flip
+    c64 = c_oracle_hist(g["cfg"], g["static"], g["forcing"], g["nsteps"], tz_name=g["tz_name"])
+    rule = flip_rule(int((flip >= 0).sum()), fp64_baseline_flips(c64, g["outputs"], 1e-10))
+    assert rule["ok"], rule
     mask = valid_mask(flip, g["nsteps"])
     for v in HIST:
         assert parity(outs[v], g["outputs"][v], mask=mask)[0] <= 1e-10, v
@@ -186,7 +192,9 @@ def test_fp32_engine_vs_oracle_on_fixture_inputs(name):
     ref, _ = oracle_run(g["cfg"], static, forcing)
     flip, genuine = melt_out_flips(outs, ref, 1e-5)
     assert not genuine, genuine
-    assert (flip >= 0).sum() <= 2, flip
+    rule = flip_rule(int((flip >= 0).sum()),
+                     fp64_baseline_flips(c_oracle_hist(g["cfg"], static, forcing, g["nsteps"]), ref))
+    assert rule["ok"], rule
     mask = valid_mask(flip, g["nsteps"])
     for v in HIST:
         err, frac = parity(outs[v], ref[v], mask=mask)
@@ -352,6 +360,7 @@ def oracle_year():
     m = O.OracleGrid(BASE_CFG, **static)
     jd, _, _, tsn = O.oracle_clock(BASE_CFG["start_time"], BASE_CFG["dt"], YEAR_STEPS, BASE_CFG["lon"])
     snaps, refs, daily = {}, {}, {v: [] for v in HIST}
+    runoff = np.zeros(YEAR_N)
     for k in range(YEAR_STEPS):
         if k in checkpoints:
             snaps[k] = {a: np.array(getattr(m, a), copy=True) for a in
@@ -361,12 +370,20 @@ def oracle_year():
         if k in checkpoints:
             refs[k] = {v: np.array(r[v], copy=True) for v in HIST}
             refs[k]["h_swe"], refs[k]["h_iwe"] = m.h_swe.copy(), m.h_iwe.copy()
+        runoff += np.asarray(r["M_total"]) * (BASE_CFG["dt"] * 3600.0)
         if k % 24 == 23:
             for v in HIST:
                 daily[v].append(np.array(r[v], copy=True))
+    # the fp64 baseline (C oracle, glibc libm) over the same cells: the whole
+    # year, and one step from every checkpoint's injected state
+    forcing = {v: syn[v] for v in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    c = c_oracle_hist(BASE_CFG, static, forcing, YEAR_STEPS, frames=np.arange(YEAR_STEPS) % 24, clock=(jd, tsn))
+    c_one = {k: c_oracle_hist(BASE_CFG, static, forcing, 1, frames=np.array([k % 24]), state=snaps[k],
+                              clock=(jd, tsn), start_step=k) for k in checkpoints}
     return dict(checkpoints=checkpoints, snaps=snaps, refs=refs, daily={v: np.stack(x) for v, x in daily.items()},
                 h_swe=m.h_swe.copy(), diag=np.array([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max]),
-                diurnal=d)
+                diurnal=d, runoff=runoff, c_daily={v: c[v][23::24] for v in HIST},
+                c_runoff=c["M_total"].sum(axis=0) * (BASE_CFG["dt"] * 3600.0), c_one_step=c_one)
 
 
 @pytest.mark.gpu
@@ -401,7 +418,10 @@ def test_fp32_one_step_parity_with_state_reinjected_over_a_year(oracle_year):
     R = {v: np.stack([Y["refs"][k][v] for k in ks]) for v in Y["refs"][ks[0]]}
     flip, genuine = melt_out_flips(G, R, 1e-5)
     assert not genuine, genuine[:5]
-    assert (flip >= 0).sum() <= max(2, int(0.002 * n)), (flip >= 0).sum()
+    # fp64 baseline: the C oracle, one step from the same injected state
+    C = {v: np.concatenate([Y["c_one_step"][k][v] for k in ks]) for v in HIST}
+    rule = flip_rule(int((flip >= 0).sum()), fp64_baseline_flips(C, {v: R[v] for v in HIST}))
+    assert rule["ok"], rule
     keep = valid_mask(flip, len(ks))
     for v in HIST + ("h_swe", "h_iwe"):
         err, _ = parity(G[v], R[v], mask=keep)
@@ -415,17 +435,22 @@ def test_fp32_free_run_over_a_year(oracle_year):
     snow depth / SWE within the floored 1e-5 everywhere; RH within 1e-6;
     precipitation integrals within 1e-8 and melt integrals within 1e-5; the
     melt rate SM (E_in - Eccs cancels at melt onset) outside 1e-5 in at most
-    0.5 % of cells; ice and runoff diverge only where the reference's
-    exact-zero melt-out gate (:1424) switches at a different step, at most 5 %
-    of cells over the year."""
+    0.5 % of cells.  Ice and runoff diverge only where the reference's
+    exact-zero melt-out gate (:1424) switches at a different step: the cells
+    where they do are held to the flip rule against the fp64 baseline (the C
+    oracle's year against the numpy oracle's, same cells).  The per-cell
+    annual runoff error of those cells is reported (TFG_REPORT_DIR)."""
     Y = oracle_year
     n = YEAR_N
     e = make_engine(BASE_CFG, 1, n, "float32", n_frames=24, hist_depth=24, fuse_steps=24)
     daily = {v: [] for v in HIST}
+    runoff = np.zeros(n)
     try:
         e.fill_synthetic(YEAR_SEED, Y["diurnal"])
         for _ in range(YEAR_STEPS // 24):
             e.run(24)
+            for j in range(24):
+                runoff += e.get_field("M_total", index=j).astype(np.float64) * (BASE_CFG["dt"] * 3600.0)
             for v in HIST:
                 daily[v].append(e.get_field(v, index=23))
         h_swe, diag = e.get_field("h_swe"), e.diagnostics()[0]
@@ -434,19 +459,48 @@ def test_fp32_free_run_over_a_year(oracle_year):
     G = {v: np.stack(x) for v, x in daily.items()}
     R = Y["daily"]
 
-    def frac_cells(v):
-        g, r = G[v], R[v]
+    def diverged(A, v):
+        g, r = A[v], R[v]
         s_v = np.percentile(np.abs(r[r != 0]), 99) if np.any(r != 0) else 0.0
         err = np.abs(g - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300)
-        return float(err.max()), float((err > 1e-5).any(axis=0).mean())
+        return float(err.max()), (err > 1e-5).any(axis=0)
 
-    assert frac_cells("h_snow")[0] <= 1e-5
+    assert diverged(G, "h_snow")[0] <= 1e-5
     assert parity(h_swe, Y["h_swe"])[0] <= 1e-5
-    assert frac_cells("RH")[0] <= 1e-6
-    assert frac_cells("SM")[1] <= 0.005, frac_cells("SM")
-    assert frac_cells("h_ice")[1] <= 0.05, frac_cells("h_ice")
+    assert diverged(G, "RH")[0] <= 1e-6
+    assert diverged(G, "SM")[1].mean() <= 0.005, diverged(G, "SM")[1].mean()
+    report = {}
+    for v in ("h_ice", "IM", "M_total"):
+        g_cells, c_cells = diverged(G, v)[1], diverged(Y["c_daily"], v)[1]
+        rule = flip_rule(int(g_cells.sum()), int(c_cells.sum()))
+        assert rule["ok"], (v, rule)
+        report[v] = rule
     rel = np.abs(diag - Y["diag"]) / np.abs(Y["diag"])
     assert np.all(rel[[0, 1, 2, 5]] <= 1e-8) and rel[3] <= 1e-5 and rel[4] <= 1e-4, rel
+
+    def runoff_err(a, cells):
+        e = np.abs(a - Y["runoff"]) / np.maximum(np.abs(Y["runoff"]), 1e-300)
+        q = np.percentile(e[cells], [50, 90, 99, 100]) if cells.any() else [0.0] * 4
+        return {"cells": int(cells.sum()), "p50": float(q[0]), "p90": float(q[1]), "p99": float(q[2]),
+                "max": float(q[3]), "all_cells_max": float(e.max())}
+
+    gd, cd = diverged(G, "M_total")[1], diverged(Y["c_daily"], "M_total")[1]
+    report["annual_runoff_rel_error_diverged_cells"] = {"gpu_fp32": runoff_err(runoff, gd),
+                                                        "c_oracle_fp64": runoff_err(Y["c_runoff"], cd)}
+    report["annual_runoff_rel_error_other_cells"] = {"gpu_fp32": runoff_err(runoff, ~gd)}
+    _report("year_divergence", report)
+
+
+def _report(name, obj):
+    """Measurements a test makes, written as JSON to $TFG_REPORT_DIR when set."""
+    import json
+    import os
+
+    d = os.environ.get("TFG_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"{name}.json"), "w") as f:
+            json.dump(obj, f, indent=1)
 
 
 def test_fp64_engine_propagates_nan_forcing_like_the_reference():

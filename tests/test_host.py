@@ -4,6 +4,7 @@
 import ctypes
 import re
 import subprocess
+import sys
 from pathlib import Path
 
 import numpy as np
@@ -16,12 +17,17 @@ import tfg_oracle as O  # noqa: E402  (checker)
 
 
 # ----------------------------------------------------------------- clock
-@pytest.mark.parametrize("name", ["cat3062920_265", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter"])
+@pytest.mark.parametrize("name", ["cat3062920_265", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2",
+                                  "dt_quarter", "clock_phoenix", "clock_anchorage"])
 def test_clock_matches_reference(name):
-    from topoflow_glacier.physics.clock import StepClock
+    """The model clock (zone from lat/lon via zone_for) against the reference's
+    own clock: Pacific across DST changes and the year end, Arizona (no DST)
+    across the DST start, Alaska across the DST end."""
+    from topoflow_glacier.physics.clock import StepClock, zone_for
 
     g = load_golden(name)
     c = g["cfg"]
+    assert zone_for(c["lat"], c["lon"]) == g["tz_name"]
     clk = StepClock(c["start_time"], c["dt"], c["lat"], c["lon"])
     jd, yr, gmt, tsn = clk.calendar(0, g["nsteps"])
     assert np.array_equal(jd, g["internal"]["julian_day"][:, 0])
@@ -58,8 +64,23 @@ def test_time_zone_lookup_and_errors():
 
     assert zone_for(46.8, -121.8) == "America/Los_Angeles"
     assert zone_for(60.4, -148.9) == "America/Anchorage"  # Wolverine glacier
-    with pytest.raises(ValueError):
-        zone_for(0.0, 0.0)
+    assert zone_for(34.0, -111.5) == "America/Phoenix"  # central Arizona: no DST
+    assert zone_for(36.06, -112.14) == "America/Phoenix"  # Grand Canyon village
+    assert zone_for(43.6, -116.2) == "America/Boise"  # Boise: Mountain, not Pacific
+    assert zone_for(48.7, -113.8) == "America/Denver"  # Glacier National Park
+    assert zone_for(43.1, -109.6) == "America/Denver"  # Wind River Range
+    assert zone_for(39.0, -105.6) == "America/Denver"
+    assert zone_for(37.75, -119.6) == "America/Los_Angeles"  # Sierra Nevada
+    assert zone_for(45.37, -121.7) == "America/Los_Angeles"  # Mount Hood
+    for lat, lon in ((0.0, 0.0),
+                     (36.15, -109.6),  # Navajo Nation, Arizona: observes DST
+                     (58.3, -134.4),  # Juneau: the panhandle is not boxed (British Columbia)
+                     (61.0, -135.0),  # Yukon
+                     (46.4, -115.0),  # Idaho County: the Pacific / Mountain line
+                     (39.8, -86.2),  # Indianapolis
+                     (32.7, -114.6)):  # Yuma, Arizona, across the river from California
+        with pytest.raises(ValueError):
+            zone_for(lat, lon)
     with pytest.raises(ValueError):
         StepClock("2070010100", 1, 46.8, -121.8).calendar(0, 2)  # perihelion table 1981-2060
 
@@ -225,3 +246,37 @@ def test_ice_flow_entry_points_reject_bad_arguments_without_a_device():
     assert L.tfg_ice_flow_dmax(None, 100.0, 100.0, None, None, 0, ctypes.byref(out)) == nat.ERR_ARG
     assert L.tfg_ice_flow_edges(None, None, None, 0) == nat.ERR_ARG
     assert nat.PREV_DEPTH == -1 and (nat.FLOW_ALL, nat.FLOW_INTERIOR, nat.FLOW_EDGES) == (0, 1, 2)
+
+
+def test_library_is_built_from_these_sources():
+    """build() keys reuse on content: the in-tree library carries the sha256 of
+    exactly the sources and flags it was built from (tfg_build_info), and
+    that hash is the one these sources give now."""
+    import __graft_entry__ as G
+    from topoflow_glacier import _native
+
+    info = _native.load().tfg_build_info().decode()
+    assert f"tfg-src-sha256={G.built_hash(G.LIB)}" in info
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-cuid=tfg_engine"]
+    assert G.built_hash(G.LIB) == G.source_hash(flags), "stale _tfg.so: run __graft_entry__.build()"
+    assert _native.code_object_sha256() is not None
+
+
+def test_bmi_one_cell_path_does_not_need_torch():
+    """The per-catchment BMI path (tfg_shared_stream) must not import torch: a
+    NextGen host without it gets the no-GPU NativeError here, not ImportError."""
+    code = (
+        "import sys; sys.modules['torch'] = None\n"
+        f"sys.path[:0] = [{str(ROOT / 'topoflow-glacier_amd')!r}]\n"
+        "from topoflow_glacier import _native\n"
+        "from topoflow_glacier.bmi import bmi_topoflow_glacier as B\n"
+        "try:\n"
+        "    B._shared_stream(0)\n"
+        "except _native.NativeError as e:\n"
+        "    print('native-error', e)\n"
+        "else:\n"
+        "    print('ok')\n"
+    )
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.startswith("native-error") or r.stdout.startswith("ok"), r.stdout

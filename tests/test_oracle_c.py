@@ -22,7 +22,7 @@ from tests.harness import OUT_NAMES, load_golden, melt_out_flips, oracle_run, va
 import tfg_oracle_c as OC  # noqa: E402  (tests/harness puts oracle/ on sys.path)
 
 FIXTURES = ["cat3062920_265", "grid64", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter",
-            "satterlund", "params"]
+            "satterlund", "params", "clock_phoenix", "clock_anchorage"]
 RTOL = 1e-12
 
 
@@ -56,7 +56,7 @@ def _lib():
 @pytest.mark.parametrize("name", FIXTURES)
 def test_c_oracle_matches_reference_outputs(name):
     g = load_golden(name)
-    out, diag = OC.run_oracle_c(g["cfg"], g["static"], g["forcing"], nthreads=2)
+    out, diag = OC.run_oracle_c(g["cfg"], g["static"], g["forcing"], nthreads=2, tz_name=g["tz_name"])
     flip = _check(out, g["outputs"], max_flips=max(1, g["ncell"] // 32))
     if (flip < 0).all():  # domain integrals: each fixture cell was its own reference model
         for v in ("vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM"):
@@ -107,3 +107,30 @@ def test_c_oracle_rejects_negative_slope_and_no_snow_no_ice():
     st.update(slope=cfg["slope"], h0_snow=0.0, h0_ice=0.0, h0_swe=0.0, h0_iwe=0.0)
     out, _ = OC.run_oracle_c(cfg, st, f, 1)  # integration_test.py:192-243
     assert out["SM"][0, 0] == 0.0 and out["IM"][0, 0] == 0.0
+
+
+def test_c_oracle_resumes_from_a_numpy_oracle_state():
+    """orc_run_from: one step of the C oracle from the numpy oracle's state at
+    step 250 (depths, cold contents, albedo, days since snowfall, the 72-slot
+    window) equals the numpy oracle's own step 250 to 1e-12.  This is the fp64
+    baseline of the one-step state-reinjection GPU test."""
+    import tfg_oracle as O
+
+    from tests.harness import BASE_CFG, c_oracle_hist, synthetic_inputs
+
+    syn, _ = synthetic_inputs(20251001, 1, 256, 24)
+    static = {k: np.asarray(syn[s], np.float64) for k, s in (
+        ("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"), ("h0_snow", "h_snow"), ("h0_ice", "h_ice"),
+        ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
+    m = O.OracleGrid(BASE_CFG, **static)
+    jd, _, _, tsn = O.oracle_clock(BASE_CFG["start_time"], 1, 260, BASE_CFG["lon"])
+    names = ("P", "T_air", "Hum_sp", "P_air", "uz")
+    for k in range(251):
+        if k == 250:
+            snap = {a: np.array(getattr(m, a), copy=True) for a in
+                    ("h_swe", "h_iwe", "Eccs", "Ecci", "n", "albedo", "h_snow", "h_ice", "ring")}
+        r = m.step(*(syn[v][k % 24].astype(np.float64) for v in names), jd[k], tsn[k])
+    c = c_oracle_hist(BASE_CFG, static, {v: syn[v] for v in names}, 1, frames=np.array([250 % 24]), state=snap,
+                      clock=(jd, tsn), start_step=250)
+    for v in OUT_NAMES:
+        assert np.max(_floored(c[v][0], r[v])) <= RTOL, v

@@ -8,7 +8,7 @@ import pytest
 from tests.harness import GOLDEN, OUT_NAMES, load_golden, oracle_run
 
 FIXTURES = ["cat3062920_265", "grid64", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter",
-            "satterlund", "params"]
+            "satterlund", "params", "clock_phoenix", "clock_anchorage"]
 RTOL = 1e-12  # bit-exact here; margin for numpy SIMD paths of other host CPUs
 
 
@@ -22,7 +22,7 @@ def _rel(a, b):
 @pytest.mark.parametrize("name", FIXTURES)
 def test_oracle_matches_reference_outputs(name):
     g = load_golden(name)
-    out, m = oracle_run(g["cfg"], g["static"], g["forcing"])
+    out, m = oracle_run(g["cfg"], g["static"], g["forcing"], tz_name=g["tz_name"])
     for v in OUT_NAMES:
         assert _rel(out[v], g["outputs"][v]) <= RTOL, v
     for v in ("Q_sum", "Qn_SW", "Qn_LW", "Qh", "Qe", "Eccs", "Ecci", "albedo", "n", "p0", "T_surf", "W_p"):

@@ -6,7 +6,7 @@
 // + six outputs).  Reports GB/s for several (R, W) mixes so the measured
 // k_fused rate can be placed against what this read/write mix can reach.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_mix tools/hbm_mix.hip
-//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0] [il|pf|tb]
+//   tools/hbm_mix [cells=67108864] [steps=24] [workgroups=2048] [skew=0] [il|pf|tb|cal]
 // skew: extra cells between consecutive planes (plane stride = cells + skew),
 // to test whether power-of-two plane strides cost HBM channel balance.
 #include <hip/hip_runtime.h>
@@ -290,6 +290,20 @@ int main(int argc, char** argv) {
     run_il<6, 7, 1024>("k_fused step mix, 1024-cell block interleave", in, out, n, steps, frames);
     run<6, 7>("k_fused step mix (6 read, 7 write), planar", in, out, n, steps, frames);
     run_il<6, 7, 64>("k_fused step mix, 64-cell block interleave", in, out, n, steps, frames);
+    CHECK(hipFree(in));
+    CHECK(hipFree(out));
+    return 0;
+  }
+  if (argc > 5 && std::string(argv[5]) == "cal") {  // PMC calibration: known bytes per dispatch
+    // rocprofv3 --pmc FETCH_SIZE (or WRITE_SIZE) -- tools/hbm_mix <n> <steps> <blocks> 0 cal:
+    // each kernel instance moves exactly n*steps*4*(R or W) bytes per dispatch, so
+    // the counter / byte ratio calibrates the gfx950 correction for 4 B lanes
+    // (k_fused's width) against 16 B lanes (the guide's calibration).
+    run<7, 0>("cal read only 4 B/lane", in, out, n, steps, frames);
+    run<7, 0, 4>("cal read only 16 B/lane", in, out, n, steps, frames);
+    run<0, 7>("cal write only 4 B/lane", in, out, n, steps, frames);
+    run<0, 7, 1, true>("cal write only 4 B/lane nt", in, out, n, steps, frames);
+    run<6, 7, 1, true>("cal k_fused mix 4 B/lane nt", in, out, n, steps, frames);
     CHECK(hipFree(in));
     CHECK(hipFree(out));
     return 0;

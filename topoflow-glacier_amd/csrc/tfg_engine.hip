@@ -18,6 +18,7 @@
 // the slab into the running fp64 totals in a fixed order (bitwise
 // reproducible).
 #include <hip/hip_runtime.h>
+#include <mutex>
 
 #include <algorithm>
 #include <cmath>
@@ -1003,10 +1004,16 @@ extern "C" {
 
 int tfg_abi_version(void) { return TFG_ABI_VERSION; }
 
-const char* tfg_build_info(void) {
-  return "libtfg abi=3 arch=gfx950 (hipcc); kernels: k_fused<float|double,exact|fast,...>, "
-         "k_diag_reduce, k_fill_synthetic";
-}
+#ifndef TFG_SRC_HASH
+#define TFG_SRC_HASH "unknown"
+#endif
+// build() (__graft_entry__.py) passes the sha256 of the sources and flags; it
+// finds this string in the built library to decide whether to recompile.
+__attribute__((used)) static const char tfg_build_tag[] =
+    "libtfg abi=3 arch=gfx950 (hipcc) tfg-src-sha256=" TFG_SRC_HASH
+    "; kernels: k_fused<float|double,exact|fast,...>, k_diag_reduce, k_fill_synthetic";
+
+const char* tfg_build_info(void) { return tfg_build_tag; }
 
 int tfg_device_count(int* count) {
   if (!count) return fail(nullptr, TFG_ERR_ARG, "null count");
@@ -1131,6 +1138,31 @@ int tfg_destroy(tfg_handle* h) {
 int tfg_set_stream(tfg_handle* h, void* stream) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
+  return TFG_OK;
+}
+
+int tfg_shared_stream(int device, void** stream) {
+  // One non-blocking stream per device for the whole process, created on first
+  // use and never destroyed (handles that use it outlive no process).
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  if (!stream) return fail(nullptr, TFG_ERR_ARG, "null stream");
+  int count = 0;
+  HIPCHK(nullptr, hipGetDeviceCount(&count));
+  if (device < 0 || device >= count || device >= 64) return fail(nullptr, TFG_ERR_ARG, "device out of range");
+  std::lock_guard<std::mutex> lock(mu);
+  if (!streams[device]) {
+    int prev = 0;
+    HIPCHK(nullptr, hipGetDevice(&prev));
+    HIPCHK(nullptr, hipSetDevice(device));
+    const hipError_t e = hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking);
+    (void)hipSetDevice(prev);
+    if (e != hipSuccess) {
+      streams[device] = nullptr;
+      return fail(nullptr, TFG_ERR_HIP, "shared stream create failed");
+    }
+  }
+  *stream = streams[device];
   return TFG_OK;
 }
 

@@ -99,6 +99,7 @@ def load() -> ctypes.CDLL:
         "tfg_destroy": ([vp], i32),
         "tfg_set_stream": ([vp, vp], i32),
         "tfg_get_stream": ([vp, ctypes.POINTER(vp)], i32),
+        "tfg_shared_stream": ([i32, ctypes.POINTER(vp)], i32),
         "tfg_set_field": ([vp, i32, i32, vp, i32, i64, i32], i32),
         "tfg_get_field": ([vp, i32, i32, vp, i32, i64, i32], i32),
         "tfg_init_state": ([vp], i32),
@@ -128,6 +129,34 @@ def load() -> ctypes.CDLL:
     return L
 
 
+def elf_section(path: Path, name: str) -> bytes | None:
+    """Bytes of one section of a 64-bit little-endian ELF file (None if absent)."""
+    import struct
+
+    data = Path(path).read_bytes()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    sec = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + i * shentsize) for i in range(shnum)]
+    stroff = sec[shstrndx][4]
+    for sh_name, _typ, _flags, _addr, off, size, *_ in sec:
+        end = data.index(b"\0", stroff + sh_name)
+        if data[stroff + sh_name:end].decode() == name:
+            return data[off:off + size]
+    return None
+
+
+def code_object_sha256(path: Path | None = None) -> str | None:
+    """sha256 of the library's device code (its ``.hip_fatbin`` section: the
+    gfx950 code objects of every kernel).  PMC traffic measured on one build is
+    quoted for another only when these agree (bench.py roofline.traffic)."""
+    import hashlib
+
+    blob = elf_section(Path(path or LIB_PATH), ".hip_fatbin")
+    return hashlib.sha256(blob).hexdigest() if blob else None
+
+
 def lib() -> ctypes.CDLL:
     return load()
 
@@ -143,7 +172,7 @@ def exported_symbols() -> list[str]:
     L = load()
     return [n for n in (
         "tfg_abi_version", "tfg_build_info", "tfg_device_count", "tfg_create", "tfg_destroy",
-        "tfg_set_stream", "tfg_get_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
+        "tfg_set_stream", "tfg_get_stream", "tfg_shared_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update",

@@ -133,15 +133,18 @@ _SHARED_STREAMS: dict = {}
 
 
 def _shared_stream(device: int) -> int:
-    """One HIP stream per device for every one-cell model of the process.
+    """One HIP stream per device for every one-cell model of the process
+    (tfg_shared_stream: owned by the engine library, no torch needed).
     NextGen steps thousands of catchment instances in turn; one stream instead
     of one per instance saves ~12 us per instance-step at 500 instances
     (tests/diagnostics/bmi_many_instances.py)."""
     if device not in _SHARED_STREAMS:
-        import torch
+        import ctypes
 
-        _SHARED_STREAMS[device] = torch.cuda.Stream(device=device)  # kept alive for the process
-    return _SHARED_STREAMS[device].cuda_stream
+        s = ctypes.c_void_p()
+        nat.check(nat.lib().tfg_shared_stream(int(device), ctypes.byref(s)))
+        _SHARED_STREAMS[device] = s.value
+    return _SHARED_STREAMS[device]
 
 
 def make_engine(cfg, n_frames: int = 1, hist_depth: int = 1) -> GlacierEngine:

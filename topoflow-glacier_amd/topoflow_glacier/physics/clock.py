@@ -39,26 +39,58 @@ _TP = (
 )
 PERIHELION = {1981 + i: tuple(int(x) for x in v.split(":")) for i, v in enumerate(_TP.split())}
 
-# Coarse IANA zones for the NextGen / NWM domain (first match wins).  The
-# reference resolves the zone with timezonefinder polygons; every reference
-# config and test lies in America/Los_Angeles.
+# IANA zones by lat/lon box, for points where a box can be justified: every
+# box lies wholly inside ONE zone's territory (borders and the water or
+# neighbouring country beyond them included), so a point in it can only be in
+# that zone.  Where zones meet irregularly -- the Idaho and Oregon Pacific /
+# Mountain line, the Navajo Nation (DST) inside Arizona (no DST), the Alaska
+# panhandle against British Columbia and Yukon, the Central / Eastern line,
+# Indiana -- no box reaches, and the caller must set `time_zone`.  The
+# reference resolves the zone with timezonefinder polygons (solar_funcs.py
+# :1616-1637), which are not available offline.  (lat0, lat1, lon0, lon1).
 _ZONES = [
-    ((51.0, 72.0, -170.0, -129.0), "America/Anchorage"),
+    # Pacific: Washington (and the Idaho panhandle) north of the Columbia, west of 117.1 W
+    ((45.6, 49.0, -124.8, -117.1), "America/Los_Angeles"),
+    # Pacific: Oregon west of Malheur County
+    ((42.0, 46.3, -124.6, -119.0), "America/Los_Angeles"),
+    # Pacific: California and western Nevada, clear of Arizona (Colorado River) and Mexico
+    ((32.72, 42.0, -124.5, -115.0), "America/Los_Angeles"),
+    # Pacific: Nevada north of Lake Mead, west of West Wendover (Mountain) and Utah
+    ((36.2, 42.0, -120.0, -114.1), "America/Los_Angeles"),
+    # Mountain, DST: Utah, Colorado, Wyoming, New Mexico
+    ((37.0, 42.0, -114.05, -109.05), "America/Denver"),
+    ((37.0, 41.0, -109.05, -102.05), "America/Denver"),
+    ((41.0, 45.0, -111.05, -104.05), "America/Denver"),
+    ((32.0, 37.0, -109.05, -103.0), "America/Denver"),
+    ((31.79, 32.0, -109.05, -106.65), "America/Denver"),  # southern New Mexico, clear of Chihuahua
+    # Mountain, DST: Montana east of the Bitterroot divide, and north of 48 N east of the 116.05 W line
+    ((45.0, 49.0, -113.0, -104.05), "America/Denver"),
+    ((48.0, 49.0, -116.0, -104.05), "America/Denver"),
+    # Mountain, DST: southern Idaho and Malheur County, Oregon
+    ((42.0, 44.8, -117.0, -111.05), "America/Boise"),
+    # Arizona outside the Navajo Nation: Mountain, no DST
+    ((31.34, 34.8, -111.0, -109.05), "America/Phoenix"),
+    ((32.5, 35.0, -114.0, -111.0), "America/Phoenix"),
+    ((35.0, 37.0, -114.0, -112.0), "America/Phoenix"),
+    # Alaska west of the Yukon border (141 W) and east of the Aleutian (Adak) zone
+    ((51.2, 71.5, -169.0, -141.0), "America/Anchorage"),
     ((18.5, 23.0, -161.0, -154.0), "Pacific/Honolulu"),
-    ((32.0, 49.5, -125.0, -114.0), "America/Los_Angeles"),
-    ((31.0, 49.5, -114.0, -102.0), "America/Denver"),
-    ((25.0, 49.5, -102.0, -87.0), "America/Chicago"),
-    ((24.0, 49.5, -87.0, -66.0), "America/New_York"),
+    # Central: Texas to Minnesota, clear of the Mountain line, Mexico, Michigan and Indiana
+    ((29.0, 45.0, -99.5, -88.5), "America/Chicago"),
+    # Eastern: east of Indiana, Kentucky's and Tennessee's Central parts, south of New Brunswick
+    ((25.0, 45.0, -84.0, -67.0), "America/New_York"),
 ]
 
 
 def zone_for(lat: float, lon: float) -> str:
-    """IANA time zone for a point in the supported domain (else ValueError,
-    as the reference raises when no zone is found, SF:1629-1630)."""
+    """IANA time zone of a point inside one of the boxes above; elsewhere
+    ValueError, asking for `time_zone` (the reference raises when it finds
+    no zone, SF:1629-1630)."""
     for (la0, la1, lo0, lo1), name in _ZONES:
         if la0 <= lat <= la1 and lo0 <= lon <= lo1:
             return name
-    raise ValueError(f"Could not determine timezone for lat={lat}, lon={lon}; set `time_zone` in the config.")
+    raise ValueError(f"No unambiguous time zone for lat={lat}, lon={lon} in the built-in table; "
+                     "set `time_zone` (an IANA name) in the config.")
 
 
 def parse_time(s) -> datetime:
