@@ -1,15 +1,24 @@
-"""Parity at BASELINE.json's full size: the 8192 x 8192 fp32 grid of the bench.
+"""Parity at the BASELINE.json GPU configurations' per-GPU sizes.
 
-The oracle cannot run 67 M cells, so this checks what holds at any size:
-  * sampled parity: 2048 cells spread over the whole grid (first and last
-    cell, both sides of every 2^k cell boundary up to 2^26, random others) are
-    compared with the oracle run on the host mirror of the same synthetic
-    inputs, step by step (catches addressing faults at large plane offsets:
-    the history slots sit up to 154 GB into their buffer);
-  * water balance over the whole grid: runoff = rain + snowfall + storage loss;
+  * config 4 (the bench): 8192 x 8192, hourly, two 24-step launches;
+  * config 3: 4096 x 4096, hourly, two 24-step launches;
+  * config 5's per-GPU slab: rows 6144..8191 of the 16384 x 16384 grid over 8
+    GPUs (2048 x 16384 cells), dt = 0.25 h (a 288-slot snowfall window), 43
+    catchments, 384 steps in four 96-step launches (longer than the window,
+    so slots expire).
+
+The oracle cannot run tens of millions of cells, so each case checks what
+holds at any size:
+  * sampled parity: about 2048 cells spread over the whole shard (first and
+    last cell, both sides of every 2^k cell boundary, random others) against
+    the oracle on the host mirror of the same synthetic inputs, step by step
+    (catches addressing faults at large plane offsets), with melt-out flips
+    held to the fp64 baseline of the same cells (tests/harness.py flip_rule);
+  * water balance over the whole shard: runoff = rain + snowfall + storage loss;
+  * per-catchment mass balance (config 5): the kernel's segmented reduction
+    equals a bincount of its own per-cell outputs, per catchment, for every
+    integral (vol_P, PR, PS, SM, IM) and P_max;
   * determinism: a second run gives bit-identical state and diagnostics.
-Both runs use two launches of 24 fused steps each (48 steps) so the state also
-crosses a launch boundary.
 """
 
 import numpy as np
@@ -20,80 +29,117 @@ from tests.harness import (BASE_CFG, c_oracle_hist, flip_rule, fp64_baseline_fli
 
 pytestmark = pytest.mark.gpu
 
-NY = NX = 8192
-N = NY * NX
-STEPS, FUSE, SEED = 48, 24, 20251001
+SEED = 20251001
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
+CONFIGS = {
+    # name: (ny, nx, row0, ny_global, dt, steps, fuse, catchments)
+    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 48, 24, 0),
+    "config3_4096sq": (4096, 4096, 0, 4096, 1.0, 48, 24, 0),
+    "config5_slab_2048x16384_dt0.25_43catch": (2048, 16384, 6144, 16384, 0.25, 384, 96, 43),
+}
 
 
-def _sample_cells(rng):
+def _sample_cells(rng, n, nx):
     edges = []
-    for k in range(6, 27):
+    for k in range(6, 32):
         for c in (2 ** k - 1, 2 ** k):
-            if c < N:
+            if c < n:
                 edges.append(c)
-    edges += [0, N - 1, N // 2, NX - 1, NX, (NY - 1) * NX]
-    rest = rng.choice(N, 2048 - len(set(edges)), replace=False)
-    return np.unique(np.concatenate([np.array(edges), rest]))
+    edges += [0, n - 1, n // 2, nx - 1, nx, n - nx]
+    edges = np.unique(np.array(edges))
+    rest = rng.choice(n, 2048 - len(edges), replace=False)
+    return np.unique(np.concatenate([edges, rest]))
 
 
-def _device_field(torch, e, name, index, dtype):
-    # GlacierEngine.get_field_device orders the engine-stream copy before
-    # torch's reads (a bare tfg_get_field into a device pointer is asynchronous)
-    return e.get_field_device(name, torch.empty(N, dtype=dtype, device="cuda:0"), index=index)
+def _catchments(row0, rows, ny_global, nx, k):
+    """bench.py's block raster: 8 x 8 blocks of the global grid, ids mod k."""
+    r = (np.arange(row0, row0 + rows) * 8 // ny_global)[:, None]
+    c = (np.arange(nx) * 8 // nx)[None, :]
+    return ((r * 8 + c) % k).astype(np.int32).reshape(-1)
 
 
-def _run(torch, cells):
-    """One full-size run: returns (sampled outputs [STEPS][cells], runoff sum,
-    swe/iwe sums before and after, final h_swe on device, diagnostics)."""
+def _run(torch, cfg, shape, cells, cid):
+    """One run of a shard: sampled outputs [steps][cells], runoff sum, storage
+    sums before and after, final h_swe on device, diagnostics, and (with
+    catchments) per-catchment bincounts of the engine's own outputs."""
     from topoflow_glacier.synthetic import diurnal_table
 
-    e = make_engine(BASE_CFG, NY, NX, "float32", n_frames=24, hist_depth=FUSE, fuse_steps=FUSE)
+    ny, nx, row0, _, dt, steps, fuse, ncatch = shape
+    n = ny * nx
+    e = make_engine(cfg, ny, nx, "float32", n_frames=24, hist_depth=fuse, fuse_steps=fuse, row0=row0,
+                    n_catch=max(ncatch, 1))
+
+    def dev(name, index, dtype):
+        # get_field_device orders the engine-stream copy before torch's reads
+        return e.get_field_device(name, torch.empty(n, dtype=dtype, device="cuda:0"), index=index)
+
     try:
-        e.fill_synthetic(SEED, diurnal_table(24), nx_global=NX)
+        e.fill_synthetic(SEED, diurnal_table(24), nx_global=nx)
+        if ncatch:
+            e.set_field("catch_id", cid)
+            cid_d = torch.as_tensor(cid.astype(np.int64), device="cuda:0")
+            per = {v: torch.zeros(ncatch, dtype=torch.float64, device="cuda:0") for v in ("P", "SM", "IM")}
+            pmax = torch.zeros(ncatch, dtype=torch.float64, device="cuda:0")
+            P_frames = [dev("P", f, torch.float64) for f in range(24)]
         idx = torch.as_tensor(cells, device="cuda:0")
-        store0 = (float(_device_field(torch, e, "h_swe", 0, torch.float64).sum()),
-                  float(_device_field(torch, e, "h_iwe", 0, torch.float64).sum()))
+        store0 = (float(dev("h_swe", 0, torch.float64).sum()), float(dev("h_iwe", 0, torch.float64).sum()))
         sampled = {v: [] for v in HIST}
         runoff = 0.0
-        for _ in range(STEPS // FUSE):
-            e.run(FUSE)
+        for launch in range(steps // fuse):
+            e.run(fuse)
             e.sync()
-            for k in range(FUSE):
+            for k in range(fuse):
+                step = launch * fuse + k
                 for v in HIST:
-                    f = _device_field(torch, e, v, k, torch.float32)
+                    f = dev(v, k, torch.float32)
                     sampled[v].append(f.index_select(0, idx).cpu().numpy())
                     if v == "M_total":
                         runoff += float(f.sum(dtype=torch.float64))
-        swe1 = _device_field(torch, e, "h_swe", 0, torch.float64)
-        store1 = (float(swe1.sum()), float(_device_field(torch, e, "h_iwe", 0, torch.float64).sum()))
-        return ({v: np.stack(a).astype(np.float64) for v, a in sampled.items()}, runoff, store0, store1,
-                swe1, e.diagnostics())
+                    if ncatch and v in ("SM", "IM"):
+                        per[v].index_add_(0, cid_d, f.double())
+                if ncatch:
+                    p = P_frames[step % 24]
+                    per["P"].index_add_(0, cid_d, p)
+                    pmax = torch.maximum(pmax, torch.zeros_like(pmax).scatter_reduce(0, cid_d, p, "amax"))
+        swe1 = dev("h_swe", 0, torch.float64)
+        store1 = (float(swe1.sum()), float(dev("h_iwe", 0, torch.float64).sum()))
+        bins = None
+        if ncatch:
+            bins = {v: t.cpu().numpy() for v, t in per.items()}
+            bins["P_max"] = pmax.cpu().numpy()
+        return ({v: np.stack(a).astype(np.float64) for v, a in sampled.items()}, runoff, store0, store1, swe1,
+                e.diagnostics(), bins)
     finally:
         e.close()
 
 
-def test_full_size_grid_sampled_parity_water_balance_and_determinism():
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_full_size_sampled_parity_water_balance_and_determinism(name):
     import torch
 
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
-    cells = _sample_cells(np.random.default_rng(5))
-    gpu, runoff, s0, s1, swe1, dg = _run(torch, cells)
+    shape = CONFIGS[name]
+    ny, nx, row0, ny_global, dt, steps, fuse, ncatch = shape
+    cfg = dict(BASE_CFG, dt=dt)
+    n = ny * nx
+    cells = _sample_cells(np.random.default_rng(5), n, nx)
+    cid = _catchments(row0, ny, ny_global, nx, ncatch) if ncatch else None
+    gpu, runoff, s0, s1, swe1, dg, bins = _run(torch, cfg, shape, cells, cid)
 
     # sampled parity against the oracle on the host mirror of the same fp32 inputs
-    syn = synthetic_cells(SEED, cells, diurnal_table(24))
-    frames = np.arange(STEPS) % 24
+    syn = synthetic_cells(SEED, cells + row0 * nx, diurnal_table(24))
+    frames = np.arange(steps) % 24
     forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
     static = {k: np.asarray(syn[s], np.float64) for k, s in (("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"),
               ("h0_snow", "h_snow"), ("h0_ice", "h_ice"), ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
-    ref, _ = oracle_run(BASE_CFG, static, forcing, STEPS)
+    ref, _ = oracle_run(cfg, static, forcing, steps)
     flip, genuine = melt_out_flips(gpu, ref, 1e-5)
     assert not genuine, genuine[:5]
-    c64 = c_oracle_hist(BASE_CFG, static, {k: syn[k] for k in forcing}, STEPS, frames=frames)
+    c64 = c_oracle_hist(cfg, static, {k: syn[k] for k in forcing}, steps, frames=frames)
     rule = flip_rule(int((flip >= 0).sum()), fp64_baseline_flips(c64, ref))
     assert rule["ok"], rule
-    ok = valid_mask(flip, STEPS)
+    ok = valid_mask(flip, steps)
     for v in HIST:
         r = ref[v][ok]
         nz = np.abs(r[r != 0])
@@ -101,15 +147,28 @@ def test_full_size_grid_sampled_parity_water_balance_and_determinism():
         err = np.abs(gpu[v][ok] - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300)
         assert err.max(initial=0.0) <= 1e-5, (v, float(err.max()))
 
-    # water balance over all 67 M cells: runoff = rain + snowfall + storage loss
-    da_m2, dt = BASE_CFG["da"] * 1e6, 1
+    # water balance over the whole shard: runoff = rain + snowfall + storage loss
+    da_m2 = BASE_CFG["da"] * 1e6
+    tot = dg.sum(axis=0)
     lhs = runoff * dt * 3600 * da_m2
-    rhs = dg[0, 1] + dg[0, 2] + ((s0[0] - s1[0]) + (s0[1] - s1[1])) * da_m2
+    rhs = tot[1] + tot[2] + ((s0[0] - s1[0]) + (s0[1] - s1[1])) * da_m2
     assert abs(lhs - rhs) <= 1e-5 * abs(rhs), (lhs, rhs)
-    assert dg[0, 0] == pytest.approx(dg[0, 1] + dg[0, 2], rel=1e-6)  # P = rain + snow (fp32 per-launch partials)
+    assert tot[0] == pytest.approx(tot[1] + tot[2], rel=1e-6)  # P = rain + snow (fp32 per-launch partials)
+
+    if ncatch:
+        # the kernel's per-catchment reduction (:558-624, :1482-1494 per
+        # catchment) against bincounts of its own per-cell outputs
+        assert dg.shape[0] == ncatch
+        scale = {"P": da_m2 * dt, "SM": da_m2 * dt * 3600, "IM": da_m2 * dt * 3600}
+        for col, v in ((0, "P"), (3, "SM"), (4, "IM")):
+            want = bins[v] * scale[v]
+            got = dg[:, col]
+            assert np.all(np.abs(got - want) <= 1e-6 * np.maximum(np.abs(want), 1e-30 + np.abs(want).max() * 1e-9)), v
+        assert np.array_equal(dg[:, 5], bins["P_max"].astype(np.float64))
+        assert np.allclose(dg[:, 0], dg[:, 1] + dg[:, 2], rtol=1e-6)
 
     # determinism: a second run, bit for bit
-    gpu2, runoff2, _, _, swe2, dg2 = _run(torch, cells)
+    gpu2, runoff2, _, _, swe2, dg2, _ = _run(torch, cfg, shape, cells, cid)
     assert torch.equal(swe1, swe2) and np.array_equal(dg, dg2) and runoff == runoff2
     for v in HIST:
         assert np.array_equal(gpu[v], gpu2[v]), v
