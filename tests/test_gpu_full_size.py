@@ -4,8 +4,8 @@
   * config 3: 4096 x 4096, hourly, two 24-step launches;
   * config 5's per-GPU slab: rows 6144..8191 of the 16384 x 16384 grid over 8
     GPUs (2048 x 16384 cells), dt = 0.25 h (a 288-slot snowfall window), 43
-    catchments, 384 steps in four 96-step launches (longer than the window,
-    so slots expire).
+    catchments (256 x 256-cell blocks, ids mod 43), 384 steps in four 96-step
+    launches (longer than the window, so slots expire).
 
 The oracle cannot run tens of millions of cells, so each case checks what
 holds at any size:
@@ -51,11 +51,12 @@ def _sample_cells(rng, n, nx):
     return np.unique(np.concatenate([edges, rest]))
 
 
-def _catchments(row0, rows, ny_global, nx, k):
-    """bench.py's block raster: 8 x 8 blocks of the global grid, ids mod k."""
-    r = (np.arange(row0, row0 + rows) * 8 // ny_global)[:, None]
-    c = (np.arange(nx) * 8 // nx)[None, :]
-    return ((r * 8 + c) % k).astype(np.int32).reshape(-1)
+def _catchments(row0, rows, nx, k):
+    """256 x 256-cell blocks of the global grid, block ids mod k: every one of
+    the k catchments appears in a 2048-row slab, each in many pieces."""
+    r = ((np.arange(row0, row0 + rows) // 256) * (nx // 256))[:, None]
+    c = (np.arange(nx) // 256)[None, :]
+    return ((r + c) % k).astype(np.int32).reshape(-1)
 
 
 def _run(torch, cfg, shape, cells, cid):
@@ -77,9 +78,9 @@ def _run(torch, cfg, shape, cells, cid):
         e.fill_synthetic(SEED, diurnal_table(24), nx_global=nx)
         if ncatch:
             e.set_field("catch_id", cid)
-            cid_d = torch.as_tensor(cid.astype(np.int64), device="cuda:0")
-            per = {v: torch.zeros(ncatch, dtype=torch.float64, device="cuda:0") for v in ("P", "SM", "IM")}
-            pmax = torch.zeros(ncatch, dtype=torch.float64, device="cuda:0")
+            # per-cell sums over the run, binned by catchment once at the end
+            per = {v: torch.zeros(n, dtype=torch.float64, device="cuda:0") for v in ("P", "SM", "IM")}
+            pmax = torch.zeros(n, dtype=torch.float64, device="cuda:0")
             P_frames = [dev("P", f, torch.float64) for f in range(24)]
         idx = torch.as_tensor(cells, device="cuda:0")
         store0 = (float(dev("h_swe", 0, torch.float64).sum()), float(dev("h_iwe", 0, torch.float64).sum()))
@@ -96,17 +97,18 @@ def _run(torch, cfg, shape, cells, cid):
                     if v == "M_total":
                         runoff += float(f.sum(dtype=torch.float64))
                     if ncatch and v in ("SM", "IM"):
-                        per[v].index_add_(0, cid_d, f.double())
+                        per[v] += f.double()
                 if ncatch:
                     p = P_frames[step % 24]
-                    per["P"].index_add_(0, cid_d, p)
-                    pmax = torch.maximum(pmax, torch.zeros_like(pmax).scatter_reduce(0, cid_d, p, "amax"))
+                    per["P"] += p
+                    torch.maximum(pmax, p, out=pmax)
         swe1 = dev("h_swe", 0, torch.float64)
         store1 = (float(swe1.sum()), float(dev("h_iwe", 0, torch.float64).sum()))
         bins = None
         if ncatch:
-            bins = {v: t.cpu().numpy() for v, t in per.items()}
-            bins["P_max"] = pmax.cpu().numpy()
+            bins = {v: np.bincount(cid, weights=t.cpu().numpy(), minlength=ncatch) for v, t in per.items()}
+            pm = pmax.cpu().numpy()
+            bins["P_max"] = np.array([pm[cid == c].max() for c in range(ncatch)])
         return ({v: np.stack(a).astype(np.float64) for v, a in sampled.items()}, runoff, store0, store1, swe1,
                 e.diagnostics(), bins)
     finally:
@@ -124,7 +126,7 @@ def test_full_size_sampled_parity_water_balance_and_determinism(name):
     cfg = dict(BASE_CFG, dt=dt)
     n = ny * nx
     cells = _sample_cells(np.random.default_rng(5), n, nx)
-    cid = _catchments(row0, ny, ny_global, nx, ncatch) if ncatch else None
+    cid = _catchments(row0, ny, nx, ncatch) if ncatch else None
     gpu, runoff, s0, s1, swe1, dg, bins = _run(torch, cfg, shape, cells, cid)
 
     # sampled parity against the oracle on the host mirror of the same fp32 inputs
