@@ -79,9 +79,10 @@ def _run(torch, cfg, shape, cells, cid):
         if ncatch:
             e.set_field("catch_id", cid)
             # per-cell sums over the run, binned by catchment once at the end
-            per = {v: torch.zeros(n, dtype=torch.float64, device="cuda:0") for v in ("P", "SM", "IM")}
+            per = {v: torch.zeros(n, dtype=torch.float64, device="cuda:0") for v in ("P", "PR", "PS", "SM", "IM")}
             pmax = torch.zeros(n, dtype=torch.float64, device="cuda:0")
             P_frames = [dev("P", f, torch.float64) for f in range(24)]
+            rain = [dev("T_air", f, torch.float32) > cfg["T_rain_snow"] for f in range(24)]  # :578-604
         idx = torch.as_tensor(cells, device="cuda:0")
         store0 = (float(dev("h_swe", 0, torch.float64).sum()), float(dev("h_iwe", 0, torch.float64).sum()))
         sampled = {v: [] for v in HIST}
@@ -101,6 +102,8 @@ def _run(torch, cfg, shape, cells, cid):
                 if ncatch:
                     p = P_frames[step % 24]
                     per["P"] += p
+                    per["PR"] += torch.where(rain[step % 24], p, 0.0)
+                    per["PS"] += torch.where(rain[step % 24], 0.0, p)
                     torch.maximum(pmax, p, out=pmax)
         swe1 = dev("h_swe", 0, torch.float64)
         store1 = (float(swe1.sum()), float(dev("h_iwe", 0, torch.float64).sum()))
@@ -159,15 +162,21 @@ def test_full_size_sampled_parity_water_balance_and_determinism(name):
 
     if ncatch:
         # the kernel's per-catchment reduction (:558-624, :1482-1494 per
-        # catchment) against bincounts of its own per-cell outputs
+        # catchment) against bincounts over the catchment raster: the
+        # precipitation integrals and P_max exactly from the forcing frames;
+        # vol_SM / vol_IM integrate SM and IM before update_swe / update_iwe
+        # clamp them (exact per-catchment values against the oracle are in
+        # test_catchment_diagnostics), so here they bound the clamped outputs'
+        # volumes from above and sum to the domain totals
         assert dg.shape[0] == ncatch
-        scale = {"P": da_m2 * dt, "SM": da_m2 * dt * 3600, "IM": da_m2 * dt * 3600}
-        for col, v in ((0, "P"), (3, "SM"), (4, "IM")):
-            want = bins[v] * scale[v]
-            got = dg[:, col]
-            assert np.all(np.abs(got - want) <= 1e-6 * np.maximum(np.abs(want), 1e-30 + np.abs(want).max() * 1e-9)), v
+        for col, v in ((0, "P"), (1, "PR"), (2, "PS")):
+            want = bins[v] * (da_m2 * dt)
+            assert np.all(np.abs(dg[:, col] - want) <= 1e-6 * np.abs(want)), (v, dg[:, col], want)
         assert np.array_equal(dg[:, 5], bins["P_max"].astype(np.float64))
-        assert np.allclose(dg[:, 0], dg[:, 1] + dg[:, 2], rtol=1e-6)
+        for col, v in ((3, "SM"), (4, "IM")):
+            out_vol = bins[v] * (da_m2 * dt * 3600)
+            assert np.all(dg[:, col] >= out_vol * (1 - 1e-6)), (v, dg[:, col], out_vol)
+        assert (dg[:, 3] > 0).all() and (dg[:, 0] > 0).all()
 
     # determinism: a second run, bit for bit
     gpu2, runoff2, _, _, swe2, dg2, _ = _run(torch, cfg, shape, cells, cid)

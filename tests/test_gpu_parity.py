@@ -315,9 +315,10 @@ def test_catchment_diagnostics():
         assert _rel(diag[c, 0], vP) < 1e-6
         assert diag[c, 5] == forcing["P"][:, sel].max()
     # per-catchment melt integrals (:1482-1494): bincounts of the oracle's
-    # per-cell SM and IM, each step's volume SM * da_m2 * dt * 3600
+    # per-cell contributions SM * da_m2 * dt * 3600 (SM and IM as integrated,
+    # before update_swe / update_iwe clamp the outputs)
     for col, v in ((3, "SM"), (4, "IM")):
-        want = np.bincount(cid, weights=ref[v].sum(axis=0) * da_m2 * 1 * 3600, minlength=nc)
+        want = np.bincount(cid, weights=np.broadcast_to(getattr(m, "cell_vol_" + v), cid.shape), minlength=nc)
         assert np.all(np.abs(diag[:, col] - want) <= 1e-5 * np.maximum(np.abs(want), np.abs(want).max())), (v, diag[:, col], want)
     assert _rel(diag[:, 3].sum(), m.vol_SM) < 1e-5
     assert _rel(diag[:, 4].sum(), m.vol_IM) < 1e-5

@@ -31,6 +31,10 @@ def test_oracle_matches_reference_outputs(name):
     for i, v in enumerate(("vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM")):
         assert _rel(out[v], g["internal"][v].sum(axis=1)) <= 1e-12, v
     assert _rel(out["P_max"], g["internal"]["P_max"].max(axis=1)) == 0.0
+    # per-cell melt integrals (the terms a catchment's vol_SM / vol_IM sum):
+    # each fixture cell was its own reference model, so they are its vol_SM / vol_IM
+    assert _rel(np.broadcast_to(m.cell_vol_SM, (g["ncell"],)), g["internal"]["vol_SM"][-1]) <= 1e-12
+    assert _rel(np.broadcast_to(m.cell_vol_IM, (g["ncell"],)), g["internal"]["vol_IM"][-1]) <= 1e-12
 
 
 def test_reference_known_answer_runoff():
