@@ -215,7 +215,7 @@ def pmc_traffic(rows, args):
     measured = prof.get("code_object_sha256")
     src = {"profile": str(pmc.relative_to(ROOT)), "code_object_sha256": measured,
            "running_code_object_sha256": running, "match": measured is not None and measured == running,
-           "read_scale": (prof.get("correction") or {}).get("read_scale")}
+           "read_scale": corr.get("read_scale") if isinstance(corr := prof.get("correction"), dict) else None}
     return (prof.get("hbm_bytes_per_launch") if src["match"] else None), src
 
 
