@@ -83,8 +83,9 @@ def main():
         "code_object_sha256": code_object_sha256(),
         "correction": {
             "read_scale": rd_scale, "write_scale": wr_scale,
-            "source": "measured on this box: tools/hbm_mix cal kernels with known bytes, 4 B lanes (k_fused's width); "
-                      "the guide's x2 FETCH_SIZE correction is calibrated for 16 B lanes",
+            "source": "measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch. FETCH_SIZE "
+                      "reports half the streamed read bytes at 4 B lanes (k_fused's width) as at 16 B lanes (the "
+                      "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes",
             "calibration": cal,
         },
         "hbm_read_bytes_per_launch": rd,
