@@ -156,9 +156,9 @@ def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
 # the last bit flip some cells.  The yardstick is the fp64 baseline of the same
 # cells and steps: the C oracle (glibc libm) against the numpy oracle (numpy's
 # SIMD libm, bit-exact to the reference fixtures) -- two fp64 restatements of
-# the same operation order.  Measured ratio GPU fp32 / fp64 baseline: 1.93 on
-# bench.py's sample (4157 / 2149 of 262 144 cells x 96 steps) and 1.9 on the
-# year-long run (ice divergence 3.5 % / 1.8 % of 2048 cells); DESIGN.md section 3.
+# the same operation order.  Measured ratio GPU fp32 / fp64 baseline: 1.94 on
+# bench.py's sample (4174 / 2149 of 262 144 cells x 96 steps) and 2.0 on the
+# year-long run (ice divergence in 74 / 37 of 2048 cells); DESIGN.md section 3.
 FLIP_RATIO_MAX = 3.0
 FLIP_SLACK = 3  # absolute allowance for samples whose baseline is a handful of cells
 
