@@ -12,7 +12,8 @@ no output write can be absorbed by a cache rewrite).
 Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
 HBM-resident frames, fp32 engine (fp64 state), 96 steps per launch (HBM
 footprint ~210 GB of the 288 GB: 24 forcing frames 32 GB, 96 output slots
-155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).
+155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).  Shards of
+2^25 cells or fewer (the N >= 2 slabs) fuse 192 steps per launch (auto_fuse).
 
 --gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
 is row-partitioned over the N ranks (strong scaling, BASELINE config 4: 1024 x
@@ -21,7 +22,9 @@ There is no data-path collective; value = all cells x steps / max-over-ranks
 time between barriers.
 
 The timed region is a whole number of fused launches, at least MIN_LAUNCHES,
-covering --steps; the JSON carries `steps_requested` beside the timed `steps`.
+covering --steps, and (with the automatic depth) a multiple of 192 steps, so
+every N times the same steps of the same grid; the JSON carries
+`steps_requested` beside the timed `steps`.
 
 Prints ONE JSON line on rank 0.  Roofline: achieved = algorithmic bytes per
 fused launch / mean launch time (HIP events on the engine's stream); traffic
@@ -52,6 +55,26 @@ BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs
 BYTES_PER_LAUNCH = 20 + (6 * 8 + 8) * 2  # solar geometry 5xf32; state 6xf64 + window total i64, in and out
 
 MIN_LAUNCHES = 3
+# auto launch depth: 96 steps for shards above 2^25 cells (the 8192^2 grid: the
+# 96 output slots already take 155 GB of HBM), 192 below (the strong-scaling
+# slabs: a deeper launch amortises the state-in / state-out phases of each
+# launch; 1024 x 8192 cells 106 -> 112 G cell-updates/s, profiles/r2_fuse_slabs.json)
+FUSE_BIG, FUSE_SMALL, FUSE_SPLIT_CELLS = 96, 192, 1 << 25
+STEP_QUANTUM = 192  # timed steps are a multiple of both depths: the same total work at every N
+
+
+def auto_fuse(cells: int) -> int:
+    return FUSE_BIG if cells > FUSE_SPLIT_CELLS else FUSE_SMALL
+
+
+def timed_steps(requested: int, fuse: int, explicit: bool) -> int:
+    """Whole launches covering `requested`, at least MIN_LAUNCHES of them.  With
+    the automatic depth the count is a multiple of STEP_QUANTUM and at least
+    MIN_LAUNCHES x 192, so N = 1 (96-step launches) and N > 1 (192-step
+    launches) time the same number of steps of the same grid."""
+    if explicit:
+        return max(MIN_LAUNCHES, -(-requested // fuse)) * fuse
+    return max(MIN_LAUNCHES, -(-requested // STEP_QUANTUM)) * STEP_QUANTUM
 
 BASE_CFG = {
     "site_prefix": "synthetic", "forcing_file": "synthetic", "dt": 1, "start_time": "2013032000",
@@ -69,7 +92,8 @@ def parse():
     ap.add_argument("--ny", type=int, default=8192, help="global rows (strong) or rows per GPU (weak)")
     ap.add_argument("--nx", type=int, default=8192)
     ap.add_argument("--frames", type=int, default=24)
-    ap.add_argument("--fuse", type=int, default=96, help="steps per launch (= output history slots)")
+    ap.add_argument("--fuse", type=int, default=0,
+                    help="steps per launch (= output history slots); 0 = by shard size (auto_fuse)")
     ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default: one --ny x --nx grid row-partitioned over the ranks, BASELINE "
@@ -197,7 +221,7 @@ def shard_plan(args, world: int, rank: int) -> dict:
         ny_global = args.ny
         row0, rows = row_block(args.ny, rank, world)
     rows_max = max(row_block(ny_global, r, world)[1] for r in range(world)) if scaling == "strong" else rows
-    return {"scaling": scaling, "ny_global": ny_global, "row0": row0, "rows": rows,
+    return {"scaling": scaling, "ny_global": ny_global, "row0": row0, "rows": rows, "rows_max": rows_max,
             "workload": f"{ny_global}x{args.nx} grid ({rows_max}x{args.nx} per GPU)"}
 
 
@@ -285,6 +309,9 @@ def main():
     plan = shard_plan(args, world, rank)
     args.scaling = plan["scaling"]
     ny_global, row0, rows = plan["ny_global"], plan["row0"], plan["rows"]
+    fuse_explicit = args.fuse > 0
+    if not fuse_explicit:  # by the largest shard, so every rank fuses alike
+        args.fuse = auto_fuse(plan["rows_max"] * args.nx)
     cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
     n_catch = args.catchments + 1 if args.catchments > 0 else 1
     eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
@@ -307,8 +334,8 @@ def main():
     # Whole fused launches, and at least MIN_LAUNCHES of them, so that a short
     # --steps still gives a multi-launch timed region; the JSON carries the
     # requested count beside the timed one.
-    n_launch = max(MIN_LAUNCHES, -(-args.steps // args.fuse))
-    steps = n_launch * args.fuse
+    steps = timed_steps(args.steps, args.fuse, fuse_explicit)
+    n_launch = steps // args.fuse
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
     barrier()
     t0 = time.perf_counter()
@@ -363,9 +390,11 @@ def main():
             "steps": steps,
             "steps_requested": args.steps,
             "steps_note": None if steps == args.steps else (
-                f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps, at least {MIN_LAUNCHES} "
-                f"launches) to cover the {args.steps} requested: a launch keeps each cell's state in registers "
-                f"across its {args.fuse} steps, so the timed region is a whole number of launches"),
+                f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps) to cover the "
+                f"{args.steps} requested: a launch keeps each cell's state in registers across its steps, so the "
+                f"timed region is a whole number of launches, at least {MIN_LAUNCHES}"
+                + ("" if fuse_explicit else f", and a multiple of {STEP_QUANTUM} steps so that every GPU count "
+                                            f"times the same work")),
             "launches": {"count": n_launch, "steps_each": args.fuse, "ms_min": float(launch_ms.min()),
                          "ms_mean": float(launch_ms.mean()), "ms_max": float(launch_ms.max())},
             "warmup": args.warmup,

@@ -37,6 +37,18 @@ def test_default_shard_plan_is_config4_strong_scaling(world):
     assert plans[0]["scaling"] == "strong"  # one label for the driver's whole N = 1, 2, 4, 8 series
 
 
+@pytest.mark.parametrize("world,fuse", [(1, 96), (2, 192), (4, 192), (8, 192)])
+def test_driver_command_times_the_same_work_at_every_n(world, fuse):
+    """`--steps 20`: whole launches, >= 3, and the same 576 steps at every N
+    (96-step launches for the whole 8192^2 grid, 192-step ones for the slabs)."""
+    bench, args = _args("--gpus", str(world), "--steps", "20", "--warmup", "5")
+    plan = bench.shard_plan(args, world, 0)
+    k = bench.auto_fuse(plan["rows_max"] * args.nx)
+    steps = bench.timed_steps(args.steps, k, explicit=False)
+    assert k == fuse and steps == 576 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
+    assert bench.timed_steps(48, 24, explicit=True) == 72  # an explicit --fuse: >= 3 launches of it
+
+
 def test_weak_scaling_stays_behind_its_flag():
     bench, args = _args("--gpus", "4", "--scaling", "weak")
     p = [bench.shard_plan(args, 4, r) for r in range(4)]
