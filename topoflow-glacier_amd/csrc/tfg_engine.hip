@@ -1558,8 +1558,24 @@ int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n
   return TFG_OK;
 }
 
+#ifdef TFG_UPDATE_TIMING
+// Diagnostic build only (tests/diagnostics/bmi_many_instances.py): where the
+// time of tfg_update goes, summed over calls [ns]: input packing, the launch
+// call, waiting for the release flags, output unpacking; [4] = calls.
+static double g_upd_ns[5];
+extern "C" void tfg_update_timing(double* out) {
+  for (int i = 0; i < 5; ++i) out[i] = g_upd_ns[i];
+}
+#define TFG_TSTAMP(v) const auto v = std::chrono::steady_clock::now()
+#define TFG_TACC(i, a, b) (g_upd_ns[i] += std::chrono::duration<double, std::nano>((b) - (a)).count())
+#else
+#define TFG_TSTAMP(v)
+#define TFG_TACC(i, a, b)
+#endif
+
 int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
                int dst_dtype, int64_t n) {
+  TFG_TSTAMP(t_in0);
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!src || !dst) return fail(h, TFG_ERR_ARG, "null src/dst");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
@@ -1605,12 +1621,16 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
     }
   }
   std::memcpy(h->io_h + u_off, u, sizeof(tfg_uniforms));
+  TFG_TSTAMP(t_in1);
+  TFG_TACC(0, t_in0, t_in1);
   IoArgs io;
   io.in = h->io_d;
   io.out = reinterpret_cast<double*>(h->io_d + out_off);
   io.flag = reinterpret_cast<uint32_t*>(h->io_d + flag_off);
   io.seq = ++h->io_seq == 0 ? ++h->io_seq : h->io_seq;  // never 0, the initial flag value
   if (int rc = launch_steps(h, reinterpret_cast<const tfg_uniforms*>(h->io_d + u_off), u, 1, io)) return rc;
+  TFG_TSTAMP(t_l1);
+  TFG_TACC(1, t_in1, t_l1);
   // Wait for the workgroups' release flags (a few microseconds sooner than a
   // stream synchronisation); after ~2 ms fall back to the stream wait, which
   // also reports a failed launch.
@@ -1626,9 +1646,16 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
     if (done) std::atomic_thread_fence(std::memory_order_acquire);
     else HIPCHK(h, hipStreamSynchronize(h->stream));
   }
+  TFG_TSTAMP(t_w1);
+  TFG_TACC(2, t_l1, t_w1);
   const double* oh = reinterpret_cast<const double*>(h->io_h + out_off);
   if (dst_dtype == TFG_F64) std::memcpy(dst, oh, out_b);
   else for (int64_t i = 0; i < 8 * n; ++i) static_cast<float*>(dst)[i] = (float)oh[i];
+  TFG_TSTAMP(t_o1);
+  TFG_TACC(3, t_w1, t_o1);
+#ifdef TFG_UPDATE_TIMING
+  g_upd_ns[4] += 1;
+#endif
   return TFG_OK;
 }
 

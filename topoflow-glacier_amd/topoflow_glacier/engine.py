@@ -218,7 +218,7 @@ class GlacierEngine:
             # per-step callers (BMI update()): serve from a block computed once
             cache = getattr(self, "_ucache", None)
             if cache is None or cache[0] != b0:
-                cache = (b0, self.clock.uniforms(b0, self._UBLOCK))
+                cache = (b0, self.clock.uniform_block(b0, self._UBLOCK))
                 self._ucache = cache
             u = cache[1][k0 - b0:k0 - b0 + nsteps]
             if default_frames and self.n_frames == 1 and self.hist_depth == 1:
@@ -255,7 +255,7 @@ class GlacierEngine:
             b0 = k0 - k0 % self._UBLOCK
             cache = getattr(self, "_ucache", None)
             if cache is None or cache[0] != b0:
-                cache = (b0, self.clock.uniforms(b0, self._UBLOCK))
+                cache = (b0, self.clock.uniform_block(b0, self._UBLOCK))
                 self._ucache = cache
             uptr = cache[1].ctypes.data + (k0 - b0) * nat.UNIFORM_DTYPE.itemsize
             keep = None

@@ -17,6 +17,7 @@ offline).
 
 from __future__ import annotations
 
+from collections import OrderedDict
 from datetime import datetime, timedelta
 from functools import lru_cache
 from zoneinfo import ZoneInfo
@@ -130,6 +131,10 @@ def _equation_of_time_hours(JD: np.ndarray, years: np.ndarray) -> np.ndarray:
     return TE / (np.float64(2) * np.pi / np.float64(24))
 
 
+_BLOCKS: "OrderedDict[tuple, np.ndarray]" = OrderedDict()  # StepClock.uniform_block, least recently used first
+_BLOCKS_MAX = 256  # blocks of 512 records (80 KB each)
+
+
 class StepClock:
     """Uniform scalars for model steps k = 0, 1, 2, ... of one run."""
 
@@ -176,6 +181,27 @@ class StepClock:
         return jd, yr, gmt, clock_hour - solar_noon
 
     # -- per-step uniforms --------------------------------------------------
+    def key(self) -> tuple:
+        """Everything the uniforms depend on: equal keys give equal records."""
+        return (self.start, float(self.dt), float(self.lat), float(self.lon), self.tz.key, self.ring_len)
+
+    def uniform_block(self, b0: int, n: int) -> np.ndarray:
+        """uniforms(b0, n) with frame = hist = 0, read-only and shared by every
+        clock of the process with the same key (NextGen runs one model per
+        catchment: an ensemble, or catchments that share a centroid clock,
+        then compute each block once, not once per model)."""
+        k = (self.key(), int(b0), int(n))
+        u = _BLOCKS.get(k)
+        if u is None:
+            u = self.uniforms(b0, n)
+            u.flags.writeable = False
+            _BLOCKS[k] = u
+            if len(_BLOCKS) > _BLOCKS_MAX:
+                _BLOCKS.popitem(last=False)
+        else:
+            _BLOCKS.move_to_end(k)
+        return u
+
     def uniforms(self, k0: int, n: int, frames=None, hist=None) -> np.ndarray:
         """tfg_uniforms records for steps k0..k0+n-1.
 
