@@ -2,7 +2,7 @@
 # on tests/diagnostics/ice_flow_timing.py at 8192^2.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_flow
+OUT=gpurun_out/${TAG:-pmc_flow}
 mkdir -p $OUT
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do

@@ -1745,12 +1745,13 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
   const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)((h->ny + kFlowRows - 1) / kFlowRows));
   if (fgrid.y > 65535u) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
   const int64_t gb = (int64_t)fgrid.x * fgrid.y;
+  const FlowTiles ft = flow_tiles(h->nx, (int)fgrid.y);
   const FlowK fk = flow_constants(1.0, dx, dy, h->dp.wi, h->flow_gamma);  // dt unused by the bound
   if (!h->flow_red) HIPCHK(h, hipMalloc((void**)&h->flow_red, (size_t)gb * 8));  // the grid never changes
   if (h->engine == TFG_F32)
-    hipLaunchKernelGGL((k_ice_flow<float, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr);
+    hipLaunchKernelGGL((k_ice_flow<float, true>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr, ft);
   else
-    hipLaunchKernelGGL((k_ice_flow<double, true>), fgrid, kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr);
+    hipLaunchKernelGGL((k_ice_flow<double, true>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, h->flow_red, 0, 1, nullptr, ft);
   HIPCHK(h, hipGetLastError());
   std::vector<double> bm(gb);
   HIPCHK(h, hipMemcpyAsync(bm.data(), h->flow_red, (size_t)gb * 8, hipMemcpyDeviceToHost, h->stream));
@@ -1785,11 +1786,11 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
   // new h_iwe goes to scratch, since neighbouring strips still read the old one
   double* ice = h->st + S_HICE * h->n_pad;
   if (count > 0) {
-    const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)count);
+    const FlowTiles ft = flow_tiles(h->nx, count);
     if (h->engine == TFG_F32)
-      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice);
+      hipLaunchKernelGGL((k_ice_flow<float, false>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice, ft);
     else
-      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice);
+      hipLaunchKernelGGL((k_ice_flow<double, false>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, h->wtmp, first, step, ice, ft);
     HIPCHK(h, hipGetLastError());
   }
   if (part == TFG_FLOW_INTERIOR) return TFG_OK;  // queued; the edges part commits
@@ -1809,7 +1810,7 @@ int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n
   const int64_t strips = (h->ny + kFlowRows - 1) / kFlowRows;
   if (strips > 65535) return fail(h, TFG_ERR_ARG, "ice flow: too many rows for one shard");
   const FlowK fk = flow_constants(dt_years / n_sub, dx, dy, h->dp.wi, h->flow_gamma);
-  const dim3 fgrid((unsigned)((h->nx + kFlowTX - 1) / kFlowTX), (unsigned)strips);
+  const FlowTiles ft = flow_tiles(h->nx, (int)strips);
   // ping-pong between the state plane and the scratch plane: a sub-step that
   // lands in the state plane writes h_ice with it, so only an odd count needs
   // the commit pass at the end
@@ -1820,9 +1821,11 @@ int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n
     g.iwe = to_state ? h->wtmp : plane;
     double* dst = to_state ? plane : h->wtmp;
     if (h->engine == TFG_F32)
-      hipLaunchKernelGGL((k_ice_flow<float, false>), fgrid, kFlowTX, 0, h->stream, g, fk, dst, 0, 1, to_state ? ice : nullptr);
+      hipLaunchKernelGGL((k_ice_flow<float, false>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, dst, 0, 1,
+                         to_state ? ice : nullptr, ft);
     else
-      hipLaunchKernelGGL((k_ice_flow<double, false>), fgrid, kFlowTX, 0, h->stream, g, fk, dst, 0, 1, to_state ? ice : nullptr);
+      hipLaunchKernelGGL((k_ice_flow<double, false>), flow_blocks(ft), kFlowTX, 0, h->stream, g, fk, dst, 0, 1,
+                         to_state ? ice : nullptr, ft);
     HIPCHK(h, hipGetLastError());
   }
   if (n_sub & 1)

@@ -90,16 +90,39 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 #define TFG_FLOW_WAVES 1  // __launch_bounds__ minimum waves per SIMD
 #endif
 constexpr int kFlowTX = 256, kFlowRows = TFG_FLOW_ROWS;  // 16 and 64 rows measured no better / slower
+// XCD-aware tile order.  Workgroup L of a 1-D launch runs on XCD L mod 8 (the
+// dispatcher deals workgroups round-robin over the 8 XCDs, each with its own
+// L2), so consecutive tiles of the row-major order would sit on different
+// XCDs and every halo column would come from another XCD's L2 or from HBM.
+// Instead XCD x takes the x-th eighth of the tiles, in row-major order: left
+// and right neighbours share an L2 and run at about the same time, and so do
+// the strips above and below (gx tiles later in the same XCD's sequence).
+struct FlowTiles {
+  int gx;       // tiles per strip (columns of kFlowTX)
+  int strips;   // strips in this launch
+  int per_xcd;  // ceil(gx * strips / 8)
+};
+inline FlowTiles flow_tiles(int64_t nx, int strips) {
+  const int gx = (int)((nx + kFlowTX - 1) / kFlowTX);
+  const int64_t tiles = (int64_t)gx * strips;
+  return {gx, strips, (int)((tiles + 7) / 8)};
+}
+inline unsigned flow_blocks(const FlowTiles& ft) { return 8u * (unsigned)ft.per_xcd; }
+
 template <class R, bool DMAX>
 __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
-                                                      int strip0, int strip_step, double* __restrict__ out_ice) {
+                                                      int strip0, int strip_step, double* __restrict__ out_ice,
+                                                      const FlowTiles ft) {
 #pragma clang fp contract(off)
   __shared__ double sS[4][kFlowTX + 2], sH[4][kFlowTX + 2];  // index k = column - (c0 - 1)
   __shared__ double red[DMAX ? kFlowTX : 1];
+  const int64_t tile = (int64_t)(blockIdx.x % 8) * ft.per_xcd + blockIdx.x / 8;
+  if (tile >= (int64_t)ft.gx * ft.strips) return;  // the padding of the last eighth (whole workgroup)
+  const int64_t tx = tile % ft.gx, ty = tile / ft.gx;
   double dmax = 0.0;
   const int t = threadIdx.x;
-  const int64_t c0 = (int64_t)blockIdx.x * kFlowTX;
-  const int64_t r0 = ((int64_t)strip0 + (int64_t)blockIdx.y * strip_step) * kFlowRows;  // this workgroup's strip
+  const int64_t c0 = tx * kFlowTX;
+  const int64_t r0 = ((int64_t)strip0 + ty * strip_step) * kFlowRows;  // this workgroup's strip
   const int64_t r1 = r0 + kFlowRows < g.ny ? r0 + kFlowRows : g.ny;
   const int64_t c = c0 + t;
   auto slot = [&](int64_t rr) { return (int)(rr - r0 + 1) & 3; };
@@ -234,7 +257,7 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
       if (t < w) red[t] = fmax(red[t], red[t + w]);
       __syncthreads();
     }
-    if (t == 0) out[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+    if (t == 0) out[tile] = red[0];  // tile = ty * gx + tx
   }
 }
 
