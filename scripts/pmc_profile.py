@@ -24,7 +24,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "topoflow-glacier_amd"))
 from topoflow_glacier._native import code_object_sha256  # noqa: E402
 
-BYTES_PER_STEP, BYTES_PER_LAUNCH = 52, 132  # bench.py / DESIGN.md section 5
+sys.path.insert(0, str(ROOT))
+from bench import launch_bytes_per_cell  # noqa: E402  
 
 
 def per_dispatch(paths, match):
@@ -74,7 +75,7 @@ def main():
     wr_scale = 1.0 / cal["write only 4 B/lane nt"]["counter_over_known"] if "write only 4 B/lane nt" in cal else 1.0
     rd = raw["FETCH_SIZE"] * 1024 * rd_scale
     wr = raw["WRITE_SIZE"] * 1024 * wr_scale
-    alg = nx * ny * (BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH)
+    alg = nx * ny * launch_bytes_per_cell(fuse, 72)
     res = {
         "kernel": f"k_fused<float,false,false,false,1> (fp32 engine, {fuse} steps fused) at {nx}x{ny}",
         "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "

@@ -215,10 +215,11 @@ def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_de
 
 
 def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,
-                   fuse_steps: int = 24, catch_id=None, n_catch: int = 1, chunks=None):
+                   fuse_steps: int = 24, catch_id=None, n_catch: int = 1, chunks=None, window: bool = False):
     """Run the GPU engine on explicit per-step forcing (one frame per step).
 
-    Returns (dict name -> [nsteps][ncell] outputs, state dict, diagnostics)."""
+    Returns (dict name -> [nsteps][ncell] outputs, state dict, diagnostics),
+    plus the snowfall-window slots [ring_len][ncell] when `window`."""
     n = ny * nx
     eng = make_engine(cfg, ny, nx, engine, n_frames=nsteps, hist_depth=nsteps, n_catch=n_catch, fuse_steps=fuse_steps)
     try:
@@ -245,7 +246,8 @@ def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, eng
                 for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")}
         state = {name: eng.get_field(name) for name in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")}
         diag = eng.diagnostics()
-        return outs, state, diag
+        window = np.stack([eng.get_field("window", index=j) for j in range(eng.ring_len)]) if window else None
+        return (outs, state, diag, window) if window is not None else (outs, state, diag)
     finally:
         eng.close()
 

@@ -1,6 +1,7 @@
 """Parity at the BASELINE.json GPU configurations' per-GPU sizes.
 
-  * config 4 (the bench): 8192 x 8192, hourly, two 24-step launches;
+  * config 4 (the bench): 8192 x 8192, hourly, two 96-step launches (the
+    bench's shape, with the in-launch window reuse through LDS);
   * config 3: 4096 x 4096, hourly, two 24-step launches;
   * config 5's per-GPU slab: rows 6144..8191 of the 16384 x 16384 grid over 8
     GPUs (2048 x 16384 cells), dt = 0.25 h (a 288-slot snowfall window), 43
@@ -33,7 +34,7 @@ SEED = 20251001
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
 CONFIGS = {
     # name: (ny, nx, row0, ny_global, dt, steps, fuse, catchments)
-    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 48, 24, 0),
+    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 192, 96, 0),  # the bench's launch shape (window reuse in LDS)
     "config3_4096sq": (4096, 4096, 0, 4096, 1.0, 48, 24, 0),
     "config5_slab_2048x16384_dt0.25_43catch": (2048, 16384, 6144, 16384, 0.25, 384, 96, 43),
 }

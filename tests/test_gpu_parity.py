@@ -246,6 +246,28 @@ def test_fusion_is_invisible(engine):
         assert np.array_equal(a[1][v], b[1][v]) and np.array_equal(a[1][v], c[1][v]), v
 
 
+@pytest.mark.parametrize("fuse,chunks,n_catch", [(96, None, 1), (100, None, 1), (150, None, 1), (192, [192, 58], 1),
+                                                  (96, [1, 96, 96, 57], 1), (150, None, 200)])
+def test_in_launch_window_reuse_is_invisible(fuse, chunks, n_catch):
+    """Launches longer than the 72-slot window keep the slots that are read
+    back within the launch in LDS (KArgs::ring_lds, up to 36 steps, fewer when
+    many catchment bins share the LDS).  Outputs, state, diagnostics and every
+    window slot equal one launch per step, bit for bit."""
+    g = load_golden("grid64")
+    nsteps = 250
+    cid = (np.arange(64) % n_catch).astype(np.int32) if n_catch > 1 else None
+    ref = gpu_run_fields(g["cfg"], g["static"], g["forcing"], 8, 8, "float32", nsteps, fuse_steps=1, catch_id=cid,
+                         n_catch=n_catch, window=True)
+    got = gpu_run_fields(g["cfg"], g["static"], g["forcing"], 8, 8, "float32", nsteps, fuse_steps=fuse, chunks=chunks,
+                         catch_id=cid, n_catch=n_catch, window=True)
+    for v in HIST:
+        assert np.array_equal(ref[0][v], got[0][v]), v
+    for v in ref[1]:
+        assert np.array_equal(ref[1][v], got[1][v]), v
+    assert np.array_equal(ref[2], got[2])
+    assert np.array_equal(ref[3], got[3])  # all 72 window slots
+
+
 def test_row_shards_equal_whole_grid():
     """Row-block shards (row0 offsets) reproduce the unsharded grid exactly."""
     cfg = dict(BASE_CFG)
