@@ -251,8 +251,8 @@ def test_fusion_is_invisible(engine):
 def test_in_launch_window_reuse_is_invisible(fuse, chunks, n_catch):
     """Launches longer than the 72-slot window keep the slots that are read
     back within the launch in LDS (KArgs::ring_lds, up to 36 steps, fewer when
-    many catchment bins share the LDS).  Outputs, state, diagnostics and every
-    window slot equal one launch per step, bit for bit."""
+    many catchment bins share the LDS).  Outputs, state and every window slot
+    equal one launch per step, bit for bit; diagnostics to 1e-6."""
     g = load_golden("grid64")
     nsteps = 250
     cid = (np.arange(64) % n_catch).astype(np.int32) if n_catch > 1 else None
@@ -264,7 +264,9 @@ def test_in_launch_window_reuse_is_invisible(fuse, chunks, n_catch):
         assert np.array_equal(ref[0][v], got[0][v]), v
     for v in ref[1]:
         assert np.array_equal(ref[1][v], got[1][v]), v
-    assert np.array_equal(ref[2], got[2])
+    # the fp32 engine sums each cell's diagnostics in fp32 over one launch's
+    # steps, so the launch partition moves their last bits
+    assert np.allclose(ref[2], got[2], rtol=1e-6, atol=0)
     assert np.array_equal(ref[3], got[3])  # all 72 window slots
 
 
