@@ -53,19 +53,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # algorithmic bytes per cell (DESIGN.md "Bytes per cell-update")
 BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs f32
 BYTES_PER_LAUNCH = 20 + (6 * 8 + 8) * 2  # solar geometry 5xf32; state 6xf64 + window total i64, in and out
-RING_LDS_MAX = 36  # tfg_engine.hip kRingLdsMax
 
 
-def launch_bytes_per_cell(fuse: int, ring_len: int, n_catch: int = 1) -> int:
+def launch_bytes_per_cell(fuse: int) -> int:
     """Algorithmic HBM bytes per cell of one fused launch:
-    52 per step + 132 per launch, less the window slots that stay in LDS: the
-    slot step k < min(K - L, 36) writes is read back at step k + L of the same
-    launch, so neither its write nor that read crosses HBM (8 B each).  The
-    engine's rule (tfg_engine.hip ring_lds_steps) also leaves the diagnostic
-    bins their LDS: at most (40960 - 4 waves x n_catch x 48 B) / 1024 steps."""
-    room = max(40960 - 4 * n_catch * 48, 0) // 1024
-    in_lds = min(max(fuse - ring_len, 0), RING_LDS_MAX, room) if ring_len >= 2 else 0
-    return BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH - 8 * in_lds
+    52 per step + 132 per launch.  (Keeping the window slots that a launch
+    reads back itself in LDS would save 8 B per such step, but reserving the
+    LDS cost 8 % of throughput on its own: DESIGN.md section 5.)"""
+    return BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH
 
 MIN_LAUNCHES = 3
 # auto launch depth: 96 steps for shards above 2^25 cells (the 8192^2 grid: the
@@ -369,7 +364,7 @@ def main():
     diag = allreduce_diagnostics(eng.diagnostics()) if world > 1 else eng.diagnostics()
 
     mean_launch_s = float(launch_ms.mean()) / 1e3
-    bytes_launch = cells * launch_bytes_per_cell(args.fuse, int(3 * 24 / args.dt), n_catch)
+    bytes_launch = cells * launch_bytes_per_cell(args.fuse)
     achieved = bytes_launch / mean_launch_s / 1e9
     # the host-fed leg and the CPU baseline run on rank 0 at N=1 only (BASELINE contract)
     pcie = pcie_inclusive(eng, args, torch) if world == 1 and args.pcie else None

@@ -75,7 +75,7 @@ def main():
     wr_scale = 1.0 / cal["write only 4 B/lane nt"]["counter_over_known"] if "write only 4 B/lane nt" in cal else 1.0
     rd = raw["FETCH_SIZE"] * 1024 * rd_scale
     wr = raw["WRITE_SIZE"] * 1024 * wr_scale
-    alg = nx * ny * launch_bytes_per_cell(fuse, 72)
+    alg = nx * ny * launch_bytes_per_cell(fuse)
     res = {
         "kernel": f"k_fused<float,false,false,false,1> (fp32 engine, {fuse} steps fused) at {nx}x{ny}",
         "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "

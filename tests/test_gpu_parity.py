@@ -248,11 +248,11 @@ def test_fusion_is_invisible(engine):
 
 @pytest.mark.parametrize("fuse,chunks,n_catch", [(96, None, 1), (100, None, 1), (150, None, 1), (192, [192, 58], 1),
                                                   (96, [1, 96, 96, 57], 1), (150, None, 200)])
-def test_in_launch_window_reuse_is_invisible(fuse, chunks, n_catch):
-    """Launches longer than the 72-slot window keep the slots that are read
-    back within the launch in LDS (KArgs::ring_lds, up to 36 steps, fewer when
-    many catchment bins share the LDS).  Outputs, state and every window slot
-    equal one launch per step, bit for bit; diagnostics to 1e-6."""
+def test_launches_longer_than_the_window_are_invisible(fuse, chunks, n_catch):
+    """Launches longer than the 72-slot window (the bench's 96 steps, the
+    slabs' 192) read back slots they wrote themselves.  Outputs, state and
+    every window slot equal one launch per step, bit for bit; diagnostics to
+    1e-6 (fp32 per-launch partial sums)."""
     g = load_golden("grid64")
     nsteps = 250
     cid = (np.arange(64) % n_catch).astype(np.int32) if n_catch > 1 else None

@@ -79,16 +79,7 @@ struct KArgs {
   double* io_out;
   uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
   uint32_t io_seq;
-  // In-launch window reuse (fast engine, K > ring_len L, consecutive slots):
-  // the slot written at step k < ring_lds is read back at step k + L of the
-  // same launch and overwritten there, so it lives in LDS, not HBM ([ring_lds]
-  // [kBlock] int32 after the diagnostic bins).  0 = every slot through HBM.
-  int ring_lds;
-  int ring_len;
 };
-// LDS steps of in-launch window reuse at most: 36 x 256 x 4 B = 36 KB per
-// workgroup keeps 4 workgroups (4 waves per SIMD) within a CU's 160 KB.
-constexpr int kRingLdsMax = 36;
 
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
 template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
@@ -213,10 +204,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
                                                   int32_t* __restrict__ ring,      // [ring_len][n_pad]
                                                   R* __restrict__ hist,            // [hist_depth][6][n_pad]
                                                   double* __restrict__ slab) {     // [gridDim][n_catch][6]
-  extern __shared__ double lds_bins[];  // [kWaves][n_catch][6], then the in-launch window [ring_lds][kBlock]
+  extern __shared__ double lds_bins[];  // [kWaves][n_catch][6]
   const DevParams& p = a.p;
   const int nb = a.n_catch * 6;
-  int32_t* __restrict__ lds_ring = reinterpret_cast<int32_t*>(lds_bins + kWaves * nb) + threadIdx.x;
   for (int i = threadIdx.x; i < kWaves * nb; i += kBlock) lds_bins[i] = ((i % 6) == 5) ? -INFINITY : 0.0;
   __syncthreads();
   double* wbins = lds_bins + (threadIdx.x >> 6) * nb;
@@ -336,9 +326,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
         f.Q[0] = sload(fr + F_Q * n_pad, oR);
         f.PA[0] = sload(fr + F_PA * n_pad, oR);
         f.UZ[0] = sload(fr + F_UZ * n_pad, oR);
-        const int kk = (k < a.K ? k : a.K - 1) - a.ring_len;  // the step that wrote this slot, if in this launch
-        if (kk >= 0 && kk < a.ring_lds) f.q[0] = lds_ring[kk * kBlock];
-        else f.q[0] = sload(ring + (int64_t)un->slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u));
+        f.q[0] = sload(ring + (int64_t)un->slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u));
       };
       auto advance = [&](int k, const Frame& f) {
         const tfg_uniforms* up = uni + k;
@@ -364,8 +352,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
           }
         }
         const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
-        if (k < a.ring_lds) lds_ring[k * kBlock] = qn[0];  // read back at step k + L of this launch
-        else sstore(ring + (int64_t)u.slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u), qn[0]);
+        sstore(ring + (int64_t)u.slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u), qn[0]);
         R* __restrict__ h = hist + (int64_t)u.hist * kNumHist * n_pad;
         sstore(h + H_HSNOW * n_pad, oR, o_hs[0]);
         sstore(h + H_SM * n_pad, oR, o_sm[0]);
@@ -983,29 +970,11 @@ struct IoArgs {
   uint32_t seq = 0;
 };
 
-// Steps of a launch whose window slot can stay in LDS (KArgs::ring_lds): the
-// fast engine's launches whose K records use consecutive slots, so that step
-// k + L rewrites the slot step k wrote.
-int ring_lds_steps(const tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io) {
-  const int L = h->ring_len;
-  if (h->engine != TFG_F32 || io.in || K <= L || L < 2) return 0;
-  for (int k = 1; k < K; ++k)
-    if (u[k].slot != (u[0].slot + k) % L) return 0;
-  // what the diagnostic bins leave of 40 KB per workgroup (4 workgroups per CU)
-  const int64_t bins = (int64_t)kWaves * h->n_catch * 6 * 8;
-  const int64_t room = std::max<int64_t>(40960 - bins, 0) / (kBlock * 4);
-  return (int)std::min<int64_t>(std::min(K - L, kRingLdsMax), room);
-}
-
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io = IoArgs(),
-                 int ring_lds = 0) {
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io = IoArgs()) {
   KArgs a;
   a.p = h->dp;
   a.K = K;
-  a.ring_lds = ring_lds;
-  a.ring_len = h->ring_len;
-  lds += (size_t)ring_lds * kBlock * 4;
   a.io_in = io.in;
   a.io_out = io.out;
   a.io_flag = io.flag;
@@ -1391,9 +1360,8 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
-    const int rl = ring_lds_steps(h, u + k0, K, io);
-    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, rl)
-                                    : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, rl);
+    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io)
+                                    : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io);
     if (rc) return rc;
     h->depths_derived = true;
   }
