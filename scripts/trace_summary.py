@@ -15,6 +15,14 @@ rows = []
 for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(f)))
 per = defaultdict(list)
+
+
+def short(name):
+    """kernel name without its parameter list: 'k_fused<float, false, false, false, 1>'"""
+    name = name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    return name.split("(")[0][:120]
+
+
 for r in rows:
     per[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
 bench = None
@@ -23,9 +31,9 @@ for line in open(bench_log):
         bench = json.loads(line)
 fused = [(k, v) for k, v in per.items() if "k_fused<float, false, false" in k]
 res = {
-    "kernels": {k.split("(")[0][:120]: {"calls": len(v), "mean_ms": sum(v) / len(v)} for k, v in
+    "kernels": {short(k): {"calls": len(v), "mean_ms": sum(v) / len(v)} for k, v in
                 sorted(per.items(), key=lambda kv: -sum(kv[1]))},
-    "k_fused_bench_shape_ms": {k.split("(")[0]: v for k, v in fused},
+    "k_fused_bench_shape_ms": {short(k): v for k, v in fused},
 }
 if bench:
     res["bench"] = {"value": bench["value"], "launches": bench.get("launches"),
