@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 3
+#define TFG_ABI_VERSION 4
 
 /* status codes */
 enum {
@@ -84,7 +84,12 @@ enum {
    * k mod ring_len.  Setting a slot rebuilds the running total before the
    * next tfg_step. */
   TFG_ST_WINDOW = 23,
-  TFG_NUM_FIELDS = 24
+  /* lateral conduction flux Qc [W m-2] added to Q_sum (:1314) while the
+   * optional conduction term is on: written by tfg_conduction_update, or set
+   * directly (which switches the term on); zero otherwise, as the reference's
+   * Qc (:312, :936-948).  Engine element type. */
+  TFG_ST_QC = 24,
+  TFG_NUM_FIELDS = 25
 };
 
 /* Diagnostics per catchment, in this order (:558-624, :1482-1494). */
@@ -314,6 +319,35 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
  * scratch plane, so no per-sub-step commit pass is needed.  Equals n_sub
  * tfg_ice_flow_step calls bit for bit. */
 int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n_sub);
+
+/* Optional lateral heat conduction (extension): the
+ * conduction term the reference reserves in the energy balance and leaves at
+ * zero (update_conduction_heat_flux :936-948, Qc = 0 from :312; Q_sum adds Qc
+ * last, :1314).  Fourier's law between neighbouring cells, fp64:
+ *   T_snow = T0 - Eccs / (rho_snow Cp_snow h_snow),
+ *   T_ice  = T0 - Ecci / (rho_ice Cp_ice h_active_layer)   (:389-395),
+ *   Qc = sum over the 4 faces of k_snow min(h_snow, h_snow') (T_snow' - T_snow)
+ *        / d^2  [both cells snow-covered] + k_ice h_active_layer
+ *        (T_ice' - T_ice) / d^2  [both cells ice-covered],
+ * d = dx (west/east) or dy (north/south); no flux across the domain edge.
+ * The pair of cells of a face see exact negatives of one flux.  Qc is
+ * evaluated from the current state and then held by every tfg_step until the
+ * next update (operator splitting over a conduction interval; the step
+ * fusion is unchanged).
+ * Halo rows are [4][nx] fp64: T_snow, h_snow, T_ice, h_ice of the neighbour
+ * shard's row adjacent to this shard; NULL at the domain edge.  Row-block
+ * shards exchange them before each update (topoflow_glacier/sharding.py,
+ * RCCL over xGMI); the sharded Qc equals the unsharded one bit for bit.
+ *
+ * This shard's first and last rows as halo rows (first[4][nx], last[4][nx];
+ * blocking). */
+int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_device);
+/* Evaluate Qc from the current state and switch the term on (k_snow, k_ice
+ * [W m-1 K-1], dx, dy [m]); the halo rows are read before the call returns. */
+int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, const double* halo_north,
+                          const double* halo_south, int halo_on_device);
+/* Switch the term off (Qc = 0: the reference's energy balance again). */
+int tfg_conduction_off(tfg_handle* h);
 
 /* Last error message of a handle (NULL: the last create/global error). */
 const char* tfg_last_error(const tfg_handle* h);

@@ -48,6 +48,15 @@ int orc_run_from(const orc_params* c, int64_t ncell, int nsteps, const double* e
                  const int32_t* frame, const double* jd, const double* tsn, double* out_last, double* out_hist,
                  double* diag, int nthreads);
 
+/* orc_run_from with the optional lateral conduction flux Qc [W m-2] added to
+ * Q_sum (:1314): step k of cell i uses qc[(k / qc_every) * ncell + i] (one
+ * [ncell] row per conduction interval of qc_every steps); qc == NULL: Qc = 0. */
+int orc_run_from_qc(const orc_params* c, int64_t ncell, int nsteps, const double* elev, const double* slope,
+                    const double* aspect, const double* h0_snow, const double* h0_ice, const double* h0_swe,
+                    const double* h0_iwe, const double* state0, const double* ring0, const double* const* forcing,
+                    const int32_t* frame, const double* jd, const double* tsn, const double* qc, int qc_every,
+                    double* out_last, double* out_hist, double* diag, int nthreads);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

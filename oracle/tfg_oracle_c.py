@@ -50,6 +50,9 @@ def load():
         L.orc_run_from.restype = ctypes.c_int
         L.orc_run_from.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int64, ctypes.c_int] + [dp] * 9 + [
             ctypes.POINTER(dp), ctypes.POINTER(ctypes.c_int32), dp, dp, dp, dp, dp, ctypes.c_int]
+        L.orc_run_from_qc.restype = ctypes.c_int
+        L.orc_run_from_qc.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int64, ctypes.c_int] + [dp] * 9 + [
+            ctypes.POINTER(dp), ctypes.POINTER(ctypes.c_int32), dp, dp, dp, ctypes.c_int, dp, dp, dp, ctypes.c_int]
         L.orc_max_threads.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -73,12 +76,15 @@ STATE_NAMES = ["h_snow", "h_ice", "h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n
 
 
 def run_oracle_c(cfg: dict, static: dict, forcing: dict, nsteps: int | None = None, clock=None, frames=None,
-                 hist: bool = True, nthreads: int = 0, tz_name: str = "America/Los_Angeles", state=None):
+                 hist: bool = True, nthreads: int = 0, tz_name: str = "America/Los_Angeles", state=None,
+                 qc=None, qc_every: int = 1):
     """Same arguments as ``tfg_oracle.run_oracle``; forcing arrays are
     [n_frames][ncell] and step k reads frame ``frames[k]`` (default k).
     ``state``: optional mid-run state to start from instead of initialize()'s,
     a dict with the numpy oracle's attribute names (STATE_NAMES and ``ring``,
     [ncell][ring_len] oldest slot first), e.g. a snapshot of an OracleGrid.
+    ``qc``: optional lateral conduction flux [W m-2], [n_intervals][ncell]
+    (or [ncell]); step k adds row k // qc_every to Q_sum.
     Returns (outputs, diag): outputs name -> [nsteps][ncell] when ``hist``,
     else name -> [ncell] of the last step; diag name -> float."""
     L = load()
@@ -113,11 +119,18 @@ def run_oracle_c(cfg: dict, static: dict, forcing: dict, nsteps: int | None = No
         ring0 = np.ascontiguousarray(np.asarray(state["ring"], np.float64).reshape(ncell, -1))
         if ring0.shape[1] != int(3 * 24 / float(cfg["dt"])):
             raise ValueError("state ring length != int(72 / dt)")
-    rc = L.orc_run_from(ctypes.byref(p), ncell, nsteps, *(_ptr(st[k]) for k in ("elev", "slope", "aspect", "h0_snow",
-                                                                               "h0_ice", "h0_swe", "h0_iwe")),
-                        _ptr(st0), _ptr(ring0),
-                        fp, fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) if fr is not None else None,
-                        _ptr(jd), _ptr(tsn), _ptr(last), _ptr(out), _ptr(diag), int(nthreads))
+    q = None
+    if qc is not None:
+        q = np.ascontiguousarray(np.asarray(qc, np.float64).reshape(-1, ncell))
+        if q.shape[0] < (nsteps + qc_every - 1) // qc_every:
+            raise ValueError("qc needs one row per conduction interval")
+    rc = L.orc_run_from_qc(ctypes.byref(p), ncell, nsteps, *(_ptr(st[k]) for k in ("elev", "slope", "aspect",
+                                                                                  "h0_snow", "h0_ice", "h0_swe",
+                                                                                  "h0_iwe")),
+                           _ptr(st0), _ptr(ring0),
+                           fp, fr.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) if fr is not None else None,
+                           _ptr(jd), _ptr(tsn), _ptr(q), int(qc_every), _ptr(last), _ptr(out), _ptr(diag),
+                           int(nthreads))
     if rc == ORC_ERR_SLOPE:
         raise ValueError("some slope angles are out of range (bmi_topoflow_glacier.py:1106-1111)")
     if rc != 0:

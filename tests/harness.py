@@ -173,7 +173,7 @@ def flip_rule(flips: int, fp64_flips: int) -> dict:
 
 
 def c_oracle_hist(cfg: dict, static: dict, forcing: dict, nsteps: int, frames=None, state=None, clock=None,
-                  start_step: int = 0, tz_name: str = "America/Los_Angeles"):
+                  start_step: int = 0, tz_name: str = "America/Los_Angeles", qc=None, qc_every: int = 1):
     """The C oracle (fp64, glibc libm) over the same cells and steps as a numpy
     oracle run: per-step outputs [nsteps][ncell].  `forcing` is [n_frames][ncell]
     per field and step k reads frames[k] (default k); `state` starts it from a
@@ -188,7 +188,8 @@ def c_oracle_hist(cfg: dict, static: dict, forcing: dict, nsteps: int, frames=No
     tsn = np.asarray(tsn)[start_step:start_step + nsteps]
     st = {k: np.asarray(static[k], np.float64) for k in STATIC_KEYS}
     f = {k: np.ascontiguousarray(np.asarray(v, np.float64)) for k, v in forcing.items()}
-    out, _ = OC.run_oracle_c(cfg, st, f, nsteps, clock=(jd, tsn), frames=frames, hist=True, state=state)
+    out, _ = OC.run_oracle_c(cfg, st, f, nsteps, clock=(jd, tsn), frames=frames, hist=True, state=state, qc=qc,
+                             qc_every=qc_every)
     return out
 
 
@@ -198,6 +199,41 @@ def fp64_baseline_flips(c_out: dict, ref: dict, rtol: float = 1e-5) -> int:
     flip, genuine = melt_out_flips({v: c_out[v] for v in names}, {v: ref[v] for v in names}, rtol)
     assert not genuine, f"C oracle vs numpy oracle: {genuine[:5]}"
     return int((flip >= 0).sum())
+
+
+# Melt onset in the fp32 engine.  SM = E_rem / (dt rho_H2O Lf) with E_rem =
+# max(Q_sum dt - Eccs, 0) (:1364-1368): where the step's energy just exceeds the
+# cold content the difference cancels.  Both sides of it carry the error of
+# the fp32 flux terms (a few 1e-7 of their magnitude: hardware exp2/log2/rcp,
+# polynomial atan; mean bias -4e-8): E_in of this step, and
+# Eccs, which integrates E_in over the steps before.  Such a mismatch is
+# explained when SM and M_total (:1441) differ by no more than 1e-6 of the
+# energy moved so far, sum over steps <= k of |Qn_SW| + |Qn_LW| + |Qh| + |Qe|,
+# in melt-rate units (E / (dt rho_H2O Lf) per step of E = Q dt); the cell is
+# then compared up to that step, like a melt-out flip.  At most ONSET_FRAC_MAX
+# of the cells may need it (the year-long test measures 0.2 % for SM).
+ONSET_FRAC_MAX = 0.005
+
+
+def melt_onsets(gpu: dict, ref: dict, genuine: list, cfg: dict) -> tuple[dict, list]:
+    """Split genuine failures into explained melt onsets {cell: step} and the rest."""
+    c = dict(O.CFG_DEFAULTS)
+    c.update(cfg)
+    rho_lf = float(c["rho_H2O"]) * float(c["Lf"])
+    onset, rest = {}, []
+    for cell, k, vars_ in genuine:
+        ok = bool(vars_) and set(vars_) <= {"SM", "M_total"} and all(t in ref for t in ("Qn_SW", "Qn_LW", "Qh", "Qe"))
+        if ok:
+            moved = sum(np.abs(np.asarray(ref[t])[:k + 1, cell]).sum() for t in ("Qn_SW", "Qn_LW", "Qh", "Qe"))
+            bound = 1e-6 * float(moved) / rho_lf
+            for v in ("SM", "M_total"):
+                d = abs(float(np.asarray(gpu[v])[k, cell]) - float(np.asarray(ref[v])[k, cell]))
+                ok &= d <= bound + 1e-7 * abs(float(np.asarray(ref[v])[k, cell]))
+        if ok:
+            onset[cell] = k
+        else:
+            rest.append((cell, k, vars_))
+    return onset, rest
 
 
 def valid_mask(flip: np.ndarray, nsteps: int) -> np.ndarray:
@@ -261,9 +297,15 @@ def synthetic_inputs(seed: int, ny: int, nx: int, n_frames: int, row0: int = 0):
 
 
 def oracle_synthetic(seed: int, ny: int, nx: int, nsteps: int, n_frames: int = 24, row0: int = 0,
-                     cfg_over: dict | None = None):
+                     cfg_over: dict | None = None, cold=None, qc=None, conduction=None):
     """The oracle on the synthetic workload (host mirror of the device
-    generator) for rows row0..row0+ny-1 of a grid nx wide."""
+    generator) for rows row0..row0+ny-1 of a grid nx wide.
+
+    Optional lateral conduction (tests of tfg_conduction_*): `cold` = initial
+    (Eccs, Ecci) [ncell] replacing initialize()'s; `qc` = a fixed Qc [ncell];
+    `conduction` = dict(k_snow, k_ice, dx, dy, every): Qc re-evaluated from the
+    oracle's own state every `every` steps (conduction_restated).  The Qc rows
+    used are returned as m.qc_rows."""
     cfg = dict(BASE_CFG)
     cfg.update(cfg_over or {})
     syn, _ = synthetic_inputs(seed, ny, nx, n_frames, row0=row0)
@@ -272,7 +314,28 @@ def oracle_synthetic(seed: int, ny: int, nx: int, nsteps: int, n_frames: int = 2
     static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"],
               "h0_snow": syn["h_snow"], "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
     static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
-    return oracle_run(cfg, static, forcing, nsteps)
+    if cold is None and qc is None and conduction is None:
+        return oracle_run(cfg, static, forcing, nsteps)
+    m = O.OracleGrid(cfg, **static)
+    if cold is not None:
+        m.Eccs, m.Ecci = (np.asarray(a, np.float64).copy() for a in cold)
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], nsteps, cfg["lon"])
+    m.qc_rows = []
+    if qc is not None:
+        m.Qc = np.asarray(qc, np.float64)
+        m.qc_rows.append(m.Qc)
+    out = {}
+    for k in range(nsteps):
+        if conduction is not None and k % conduction["every"] == 0:
+            shape = (ny, nx)
+            m.Qc = conduction_restated(m.h_swe.reshape(shape), m.h_iwe.reshape(shape), m.Eccs.reshape(shape),
+                                       m.Ecci.reshape(shape), cfg, conduction["k_snow"], conduction["k_ice"],
+                                       conduction["dx"], conduction["dy"]).reshape(-1)
+            m.qc_rows.append(m.Qc)
+        r = m.step(*(forcing[n][k] for n in ("P", "T_air", "Hum_sp", "P_air", "uz")), jd[k], tsn[k])
+        for key, v in r.items():
+            out.setdefault(key, []).append(np.array(v, copy=True))
+    return {key: np.stack(v) for key, v in out.items()}, m
 
 
 def oracle_diag(m) -> np.ndarray:
@@ -281,16 +344,29 @@ def oracle_diag(m) -> np.ndarray:
 
 
 def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", seed: int = 7,
-                      n_frames: int = 24, fuse_steps: int = 24, cfg_over: dict | None = None):
+                      n_frames: int = 24, fuse_steps: int = 24, cfg_over: dict | None = None,
+                      cold=None, qc=None, conduction=None):
     """Device-generated synthetic workload on the GPU vs the oracle on the same
-    fp32 inputs (host mirror).  Returns a report dict."""
+    fp32 inputs (host mirror).  Returns a report dict.  `cold`, `qc` and
+    `conduction` switch on the optional lateral conduction term on both sides
+    (oracle_synthetic)."""
     cfg = dict(BASE_CFG)
     cfg.update(cfg_over or {})
     syn, diurnal = synthetic_inputs(seed, ny, nx, n_frames)
     eng = make_engine(cfg, ny, nx, engine, n_frames=n_frames, hist_depth=nsteps, fuse_steps=fuse_steps)
     try:
         eng.fill_synthetic(seed, diurnal)
-        eng.run(nsteps)
+        if cold is not None:
+            eng.set_field("Eccs", cold[0])
+            eng.set_field("Ecci", cold[1])
+        if qc is not None:
+            eng.set_field("Qc", qc)
+        if conduction is None:
+            eng.run(nsteps)
+        else:
+            for k0 in range(0, nsteps, conduction["every"]):
+                eng.conduction_update(conduction["k_snow"], conduction["k_ice"], conduction["dx"], conduction["dy"])
+                eng.run(min(conduction["every"], nsteps - k0))
         eng.sync()
         gpu = {name: np.stack([eng.get_field(name, index=k) for k in range(nsteps)])
                for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")}
@@ -299,23 +375,38 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
         diag = eng.diagnostics()
     finally:
         eng.close()
-    ref, m = oracle_synthetic(seed, ny, nx, nsteps, n_frames, cfg_over=cfg_over)
+    ref, m = oracle_synthetic(seed, ny, nx, nsteps, n_frames, cfg_over=cfg_over, cold=cold, qc=qc,
+                              conduction=conduction)
     static = {"elev": syn["elev"], "slope": syn["slope"], "aspect": syn["aspect"], "h0_snow": syn["h_snow"],
               "h0_ice": syn["h_ice"], "h0_swe": syn["h_swe"], "h0_iwe": syn["h_iwe"]}
+    state = None
+    if cold is not None:  # the same initial state for the C oracle, with initialize()'s window and albedo
+        m0 = O.OracleGrid(cfg, **{k: np.asarray(v, np.float64) for k, v in static.items()})
+        state = {"h_snow": m0.h_snow, "h_ice": m0.h_ice, "h_swe": m0.h_swe, "h_iwe": m0.h_iwe, "Eccs": cold[0],
+                 "Ecci": cold[1], "albedo": m0.albedo, "n": m0.n, "ring": m0.ring}
+    qc_rows = getattr(m, "qc_rows", None) or None
     c64 = c_oracle_hist(cfg, static, {k: syn[k] for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}, nsteps,
-                        frames=np.arange(nsteps) % n_frames)
+                        frames=np.arange(nsteps) % n_frames, state=state,
+                        qc=None if qc_rows is None else np.stack(qc_rows),
+                        qc_every=conduction["every"] if conduction is not None else max(nsteps, 1))
     report = {}
     worst = 0.0
     worst_rel = 0.0
     tol = 1e-5 if engine == "float32" else 1e-10
     flip, genuine = melt_out_flips(gpu, ref, tol)
-    mask = valid_mask(flip, nsteps)
+    onset = {}
+    if engine == "float32" and genuine:
+        onset, genuine = melt_onsets(gpu, ref, genuine, cfg)
+    cut = flip.copy()
+    for cell, k in onset.items():
+        cut[cell] = k
+    mask = valid_mask(cut, nsteps)
     for name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH"):
         e, frac = parity(gpu[name], ref[name], mask=mask)
         report[name] = (e, frac)
         worst = max(worst, e)
     for name in ("h_swe", "h_iwe"):
-        e, frac = parity(gpu[name], ref[name][-1], mask=flip < 0)
+        e, frac = parity(gpu[name], ref[name][-1], mask=cut < 0)
         report[name] = (e, frac)
         worst = max(worst, e)
     dref = np.array([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max])
@@ -328,13 +419,15 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     worst_rel = max(worst, report["diag"][0])
     n_flip = int((flip >= 0).sum())
     rule = flip_rule(n_flip, fp64_baseline_flips(c64, ref, tol))
-    ok = worst_rel <= tol and not genuine and rule["ok"]
+    onset_ok = len(onset) <= int(np.ceil(ONSET_FRAC_MAX * flip.size))
+    ok = worst_rel <= tol and not genuine and rule["ok"] and onset_ok
     summary = (", ".join(f"{k}={v[0]:.2e}" for k, v in report.items())
-               + f", melt-out flips={n_flip}/{flip.size} (fp64 baseline {rule['fp64_flips']}, budget {rule['budget']})")
+               + f", melt-out flips={n_flip}/{flip.size} (fp64 baseline {rule['fp64_flips']}, budget {rule['budget']})"
+               + (f", melt onsets within fp32 flux rounding={len(onset)}" if onset else ""))
     if genuine:
         summary += f", FAILURES={genuine[:5]}"
     return {"ok": ok, "max_rel": worst_rel, "report": report, "summary": summary, "gpu": gpu, "ref": ref,
-            "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine, "flip_rule": rule}
+            "diag": dg, "diag_ref": dref, "flips": n_flip, "genuine": genuine, "flip_rule": rule, "onsets": onset}
 
 
 def terrain_dem(ny: int, nx: int) -> np.ndarray:
@@ -468,3 +561,86 @@ def glacier_valley(ny: int, nx: int, dx: float = 100.0):
     bed = 3000.0 - 0.08 * dx * y + 0.002 * (x - nx / 2) ** 2 * dx
     H = np.maximum(0.0, 220.0 * (1.0 - ((x - nx / 2) / (0.35 * nx)) ** 2 - ((y - 0.4 * ny) / (0.45 * ny)) ** 2))
     return bed.astype(np.float32).astype(np.float64), H * (917.0 / 1000.0)
+
+
+# ----------------------------------------------------------------------------
+# Optional lateral heat conduction (tfg_conduction_*; extension with no
+# reference counterpart beyond the reserved Qc term, :936-948, :1314).  numpy
+# fp64 restatement of tfg_conduction.hpp, same operation order.
+# ----------------------------------------------------------------------------
+def conduction_cells(swe, iwe, eccs, ecci, cfg: dict):
+    """(T_snow, h_snow, T_ice, h_ice) per cell from the state (:389-395, :1711, :1726)."""
+    c = dict(O.CFG_DEFAULTS)
+    c.update(cfg)
+    ws = np.float64(c["rho_H2O"]) / np.float64(c["rho_snow"])
+    wi = np.float64(c["rho_H2O"]) / np.float64(c["rho_ice"])
+    inv_cs = 1.0 / (np.float64(c["rho_snow"]) * np.float64(c["Cp_snow"]))
+    inv_ci = 1.0 / ((np.float64(c["rho_ice"]) * np.float64(c["Cp_ice"])) * np.float64(c["h_active_layer"]))
+    T0 = np.float64(c["T0"])
+    hs = np.asarray(swe, np.float64) * ws
+    hi = np.asarray(iwe, np.float64) * wi
+    with np.errstate(divide="ignore", invalid="ignore"):
+        Ts = np.where(hs > 0, T0 - (np.asarray(eccs, np.float64) * inv_cs) / hs, T0)
+    Ti = np.where(hi > 0, T0 - np.asarray(ecci, np.float64) * inv_ci, T0)
+    return Ts, hs, Ti, hi
+
+
+def conduction_restated(swe, iwe, eccs, ecci, cfg: dict, k_snow: float, k_ice: float, dx: float, dy: float,
+                        north=None, south=None):
+    """Qc [W m-2] of a [ny][nx] shard; north/south halo rows [4][nx] (T_snow,
+    h_snow, T_ice, h_ice) or None at the domain edge (no flux)."""
+    c = dict(O.CFG_DEFAULTS)
+    c.update(cfg)
+    h_al = np.float64(c["h_active_layer"])
+    Ts, hs, Ti, hi = conduction_cells(swe, iwe, eccs, ecci, cfg)
+    ny, nx = Ts.shape
+
+    def padded(a, k):
+        n = np.zeros(nx) if north is None else np.asarray(north, np.float64).reshape(4, nx)[k]
+        s = np.zeros(nx) if south is None else np.asarray(south, np.float64).reshape(4, nx)[k]
+        p = np.vstack([n[None], a, s[None]])
+        return np.hstack([np.zeros((ny + 2, 1)), p, np.zeros((ny + 2, 1))])
+
+    P = [padded(a, k) for k, a in enumerate((Ts, hs, Ti, hi))]
+    gsx, gsy = k_snow / (dx * dx), k_snow / (dy * dy)
+    gix, giy = k_ice * h_al / (dx * dx), k_ice * h_al / (dy * dy)
+    qs = np.zeros((ny, nx))
+    qi = np.zeros((ny, nx))
+    for (r, cc), gs, gi in (((0, 1), gsy, giy), ((2, 1), gsy, giy), ((1, 0), gsx, gix), ((1, 2), gsx, gix)):
+        nTs, nhs, nTi, nhi = (p[r:r + ny, cc:cc + nx] for p in P)
+        ms = (hs > 0) & (nhs > 0)
+        qs = np.where(ms, qs + (np.minimum(hs, nhs) * (nTs - Ts)) * gs, qs)
+        mi = (hi > 0) & (nhi > 0)
+        qi = np.where(mi, qi + (nTi - Ti) * gi, qi)
+    return qs + qi
+
+
+class RestatedCondShard:
+    """A row-block shard of the conduction restatement with the engine's
+    conduction_* interface (for sharding.lateral_conduction on CPU)."""
+
+    def __init__(self, swe, iwe, eccs, ecci, cfg: dict):
+        self.state = [np.asarray(a, np.float64) for a in (swe, iwe, eccs, ecci)]
+        self.cfg = cfg
+        self.nx = self.state[0].shape[1]
+        self.qc = None
+
+    def conduction_edges(self):
+        cells = conduction_cells(*self.state, self.cfg)
+        return np.stack([a[0] for a in cells]), np.stack([a[-1] for a in cells])
+
+    def conduction_update(self, k_snow, k_ice, dx, dy, north=None, south=None):
+        self.qc = conduction_restated(*self.state, self.cfg, k_snow, k_ice, dx, dy, north, south)
+
+
+def conduction_state(ny: int, nx: int, seed: int = 3):
+    """A [ny][nx] state with snow-free and ice-free patches and varied cold
+    contents: h_swe, h_iwe [m w.e.], Eccs, Ecci [J m-2]."""
+    rng = np.random.default_rng(seed)
+    swe = rng.uniform(0.0, 0.5, (ny, nx))
+    swe[rng.random((ny, nx)) < 0.2] = 0.0
+    iwe = rng.uniform(0.0, 2.0, (ny, nx))
+    iwe[rng.random((ny, nx)) < 0.2] = 0.0
+    eccs = np.where(swe > 0, rng.uniform(0.0, 2.0e6, (ny, nx)), 0.0)
+    ecci = np.where(iwe > 0, rng.uniform(0.0, 1.0e6, (ny, nx)), 0.0)
+    return swe, iwe, eccs, ecci

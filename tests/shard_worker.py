@@ -24,7 +24,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain", "flow", "gpu_flow"], required=True)
+    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain", "flow", "gpu_flow", "cond", "gpu_cond"], required=True)
     ap.add_argument("--ny", type=int, required=True)
     ap.add_argument("--nx", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
@@ -85,6 +85,29 @@ def main():
         out = sh.iwe.reshape(-1) if a.mode == "flow" else sh.get_field("h_iwe")
         np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, iwe=out, n_sub=n_sub)
         if a.mode == "gpu_flow":
+            sh.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    if a.mode in ("cond", "gpu_cond"):
+        # the optional lateral conduction term over row blocks:
+        # sharding.lateral_conduction swaps the edge rows over gloo, then each
+        # shard evaluates its Qc
+        from tests.harness import BASE_CFG, RestatedCondShard, conduction_state, make_engine
+        from topoflow_glacier.sharding import lateral_conduction
+
+        swe, iwe, eccs, ecci = (x[row0:row0 + rows] for x in conduction_state(a.ny, a.nx))
+        if a.mode == "cond":
+            sh = RestatedCondShard(swe, iwe, eccs, ecci, dict(BASE_CFG))
+        else:
+            sh = make_engine(dict(BASE_CFG), rows, a.nx, "float64", n_frames=1, hist_depth=1, row0=row0)
+            sh.init_state()
+            for name, v in (("h_swe", swe), ("h_iwe", iwe), ("Eccs", eccs), ("Ecci", ecci)):
+                sh.set_field(name, v.reshape(-1))
+        lateral_conduction(sh, 0.3, 2.1, 2.0, 3.0)
+        qc = sh.qc.reshape(-1) if a.mode == "cond" else sh.get_field("Qc")
+        np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, qc=qc)
+        if a.mode == "gpu_cond":
             sh.close()
         dist.barrier()
         dist.destroy_process_group()

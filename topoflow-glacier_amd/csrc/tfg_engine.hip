@@ -33,6 +33,7 @@
 
 #include "../../include/tfg.h"
 #include "tfg_physics.hpp"
+#include "tfg_conduction.hpp"
 
 namespace {
 
@@ -193,7 +194,7 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_MIN_WAVES_EXACT
 #define TFG_MIN_WAVES_EXACT 2  // fp64 engine: 256 VGPRs, no scratch spills
 #endif
-template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, int C>
+template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C>
 __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
@@ -203,7 +204,8 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
                                                   int64_t* __restrict__ tot,       // [n_pad]
                                                   int32_t* __restrict__ ring,      // [ring_len][n_pad]
                                                   R* __restrict__ hist,            // [hist_depth][6][n_pad]
-                                                  double* __restrict__ slab) {     // [gridDim][n_catch][6]
+                                                  double* __restrict__ slab,       // [gridDim][n_catch][6]
+                                                  const R* __restrict__ qcf) {     // [n_pad] Qc [W m-2] (QC) | null
   extern __shared__ double lds_bins[];  // [kWaves][n_catch][6]
   const DevParams& p = a.p;
   const int nb = a.n_catch * 6;
@@ -297,6 +299,13 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
       }
+      // optional lateral conduction flux, held for the launch (tfg_conduction.hpp)
+      R qc[C];
+      if constexpr (QC) vload<R, C>(qcf, lc, qc);
+      else {
+#pragma unroll
+        for (int j = 0; j < C; ++j) qc[j] = (R)0;
+      }
       // fast engine: fp32 partial sums of this cell over the launch's steps
       tfg::DiagF df[EXACT ? 1 : C];
       if constexpr (!EXACT) {
@@ -339,14 +348,15 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
             CellOut o;
             CellDiag& d = CATCH ? cacc[j] : acc;
             const bool valid = (c0 + j) < a.n;
-            tfg::cell_step_exact(p, SX[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
-                                 (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid);
+            tfg::cell_step_exact<QC>(p, SX[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
+                                     (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid, (double)qc[j]);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           } else {
             tfg::CellOutF o;
-            tfg::cell_step_fast(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j], (float)f.Q[j],
-                                (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j]);
+            tfg::cell_step_fast<QC>(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j],
+                                    (float)f.Q[j], (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j],
+                                    (float)qc[j]);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           }
@@ -746,6 +756,12 @@ struct tfg_handle {
   double* flow_edges = nullptr;  // [2 rows][2][nx] f64 this shard's edge rows
   double* flow_red = nullptr;    // f64 per-workgroup maxima of k_ice_flow<R, true>
   double flow_gamma = 0.0;       // 2A/(n+2) (rho_ice g)^n, n = 3 [m^-3 yr^-1]
+  // optional lateral conduction: Qc plane (engine type) added to Q_sum while qc_on
+  void* qc = nullptr;            // [n_pad] R
+  bool qc_on = false;
+  double* cond_halo = nullptr;   // [2 sides][4][nx] f64 halo rows (T_snow, h_snow, T_ice, h_ice)
+  double* cond_edges = nullptr;  // [2 rows][4][nx] f64 this shard's edge rows
+  double inv_cs = 0.0, inv_ci = 0.0, h_active = 0.0;  // 1/(rho_s Cp_s), 1/(rho_i Cp_i h_al), h_al
   // tfg_set_inputs: pinned host staging ring (2 slots) + device staging
   void* in_h[2] = {nullptr, nullptr};
   void* in_d[2] = {nullptr, nullptr};
@@ -781,6 +797,14 @@ int fail(tfg_handle* h, int code, const std::string& msg) {
   } while (0)
 
 size_t dtype_size(int dt) { return dt == TFG_F64 ? 8 : 4; }
+
+// The Qc plane, allocated (zeroed) on first use.
+int ensure_qc(tfg_handle* h) {
+  if (h->qc) return TFG_OK;
+  HIPCHK(h, hipMalloc(&h->qc, (size_t)h->n_pad * h->rsz));
+  HIPCHK(h, hipMemsetAsync(h->qc, 0, (size_t)h->n_pad * h->rsz, h->stream));
+  return TFG_OK;
+}
 
 int ensure_staging(tfg_handle* h, size_t bytes) {
   if (bytes <= h->staging_bytes) return TFG_OK;
@@ -985,11 +1009,21 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   const bool rd = !h->depths_derived;
   const bool ct = h->catch_id != nullptr;
   constexpr int C = kCellsPerThread;
-#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, h->slab
-  if (rd && ct) hipLaunchKernelGGL((k_fused<R, EXACT, true, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
-  else if (rd) hipLaunchKernelGGL((k_fused<R, EXACT, true, false, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
-  else if (ct) hipLaunchKernelGGL((k_fused<R, EXACT, false, true, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
-  else hipLaunchKernelGGL((k_fused<R, EXACT, false, false, C>), blocks, kBlock, lds, h->stream, TFG_ARGS);
+#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, \
+                 h->slab, (const R*)h->qc
+#define TFG_LAUNCH(RD, CT, QC) hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C>), blocks, kBlock, lds, h->stream, TFG_ARGS)
+  if (h->qc_on) {  // the optional lateral conduction term (tfg_conduction_update / TFG_ST_QC)
+    if (rd && ct) TFG_LAUNCH(true, true, true);
+    else if (rd) TFG_LAUNCH(true, false, true);
+    else if (ct) TFG_LAUNCH(false, true, true);
+    else TFG_LAUNCH(false, false, true);
+  } else {
+    if (rd && ct) TFG_LAUNCH(true, true, false);
+    else if (rd) TFG_LAUNCH(true, false, false);
+    else if (ct) TFG_LAUNCH(false, true, false);
+    else TFG_LAUNCH(false, false, false);
+  }
+#undef TFG_LAUNCH
 #undef TFG_ARGS
   HIPCHK(h, hipGetLastError());
   return TFG_OK;
@@ -1010,7 +1044,7 @@ int tfg_abi_version(void) { return TFG_ABI_VERSION; }
 // build() (__graft_entry__.py) passes the sha256 of the sources and flags; it
 // finds this string in the built library to decide whether to recompile.
 __attribute__((used)) static const char tfg_build_tag[] =
-    "libtfg abi=3 arch=gfx950 (hipcc) tfg-src-sha256=" TFG_SRC_HASH
+    "libtfg abi=4 arch=gfx950 (hipcc) tfg-src-sha256=" TFG_SRC_HASH
     "; kernels: k_fused<float|double,exact|fast,...>, k_diag_reduce, k_fill_synthetic";
 
 const char* tfg_build_info(void) { return tfg_build_tag; }
@@ -1061,6 +1095,9 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   {
     const double rg = p->rho_ice * p->g;  // Glen's law n = 3: Gamma = 2A/5 (rho_ice g)^3
     h->flow_gamma = 2.0 * p->glens_A / 5.0 * (rg * rg * rg);
+    h->inv_cs = 1.0 / (p->rho_snow * p->Cp_snow);
+    h->inv_ci = 1.0 / ((p->rho_ice * p->Cp_ice) * p->h_active_layer);
+    h->h_active = p->h_active_layer;
   }
   if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TFG_ERR_HIP); }
   hipDeviceProp_t prop;
@@ -1117,7 +1154,7 @@ int tfg_destroy(tfg_handle* h) {
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
-                  h->flow_halo, h->flow_edges, h->flow_red,
+                  h->flow_halo, h->flow_edges, h->flow_red, h->qc, h->cond_halo, h->cond_edges,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
@@ -1208,6 +1245,12 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     return TFG_OK;
   }
   if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  if (field == TFG_ST_QC) {  // a caller-supplied conduction flux: on until tfg_conduction_off
+    if (int rc = ensure_qc(h)) return rc;
+    if (int rc = upload(h, h->qc, h->engine, src, src_dtype, n, src_on_device)) return rc;
+    h->qc_on = true;
+    return TFG_OK;
+  }
   if (field == TFG_ST_WINDOW) {
     if (index < 0 || index >= h->ring_len) return fail(h, TFG_ERR_ARG, "window slot out of range");
     if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
@@ -1279,6 +1322,10 @@ int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype,
     return TFG_OK;
   }
   if (dst_dtype != TFG_F32 && dst_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "dst dtype must be TFG_F32/TFG_F64");
+  if (field == TFG_ST_QC) {  // zero until a conduction pass or a set (the reference's Qc = 0, :312)
+    if (int rc = ensure_qc(h)) return rc;
+    return download(h, dst, dst_dtype, h->qc, h->engine, n, dst_on_device);
+  }
   if (field == TFG_ST_WINDOW) {
     if (index < 0 || index >= h->ring_len) return fail(h, TFG_ERR_ARG, "window slot out of range");
     if (!h->wtmp) HIPCHK(h, hipMalloc((void**)&h->wtmp, (size_t)h->n_pad * 8));
@@ -1832,6 +1879,85 @@ int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n
     hipLaunchKernelGGL(k_flow_commit<true>, grid_for(h->n), 256, 0, h->stream, h->st, h->wtmp, h->n, h->n_pad, h->dp.wi);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+namespace {
+// Conduction halos into h->cond_halo; the CondGrid of this shard.
+int cond_setup(tfg_handle* h, const double* hn, const double* hs, int on_dev, tfg::CondGrid& g) {
+  if (!h->initialised) return fail(h, TFG_ERR_STATE, "tfg_init_state() has not been called");
+  const int64_t nx = h->nx, np = h->n_pad;
+  if (!h->cond_halo) HIPCHK(h, hipMalloc((void**)&h->cond_halo, (size_t)8 * nx * 8));
+  const hipMemcpyKind k = on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+  if (hn) HIPCHK(h, hipMemcpyAsync(h->cond_halo, hn, (size_t)4 * nx * 8, k, h->stream));
+  if (hs) HIPCHK(h, hipMemcpyAsync(h->cond_halo + 4 * nx, hs, (size_t)4 * nx * 8, k, h->stream));
+  g.swe = h->st + S_HSWE * np;
+  g.iwe = h->st + S_HIWE * np;
+  g.eccs = h->st + S_ECCS * np;
+  g.ecci = h->st + S_ECCI * np;
+  g.hn = hn ? h->cond_halo : nullptr;
+  g.hs = hs ? h->cond_halo + 4 * nx : nullptr;
+  g.ny = h->ny;
+  g.nx = nx;
+  g.ws = h->dp.ws;
+  g.wi = h->dp.wi;
+  g.T0 = h->dp.T0;
+  g.inv_cs = h->inv_cs;
+  g.inv_ci = h->inv_ci;
+  return TFG_OK;
+}
+}  // namespace
+
+int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_device) {
+  if (!h || !first || !last) return fail(h, TFG_ERR_ARG, "null argument");
+  HIPCHK(h, hipSetDevice(h->device));
+  tfg::CondGrid g;
+  if (int rc = cond_setup(h, nullptr, nullptr, 0, g)) return rc;
+  const int64_t nx = h->nx;
+  if (!h->cond_edges) HIPCHK(h, hipMalloc((void**)&h->cond_edges, (size_t)8 * nx * 8));
+  hipLaunchKernelGGL(tfg::k_conduction_edges, grid_for(nx), 256, 0, h->stream, g, h->cond_edges, h->cond_edges + 4 * nx);
+  HIPCHK(h, hipGetLastError());
+  const hipMemcpyKind k = on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  HIPCHK(h, hipMemcpyAsync(first, h->cond_edges, (size_t)4 * nx * 8, k, h->stream));
+  HIPCHK(h, hipMemcpyAsync(last, h->cond_edges + 4 * nx, (size_t)4 * nx * 8, k, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+
+int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, const double* halo_north,
+                          const double* halo_south, int halo_on_device) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
+  if (!(k_snow >= 0) || !(k_ice >= 0)) return fail(h, TFG_ERR_ARG, "conductivities must be >= 0");
+  HIPCHK(h, hipSetDevice(h->device));
+  tfg::CondGrid g;
+  if (int rc = cond_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
+  if (int rc = ensure_qc(h)) return rc;
+  const tfg::CondK K = {k_snow / (dx * dx), k_snow / (dy * dy), k_ice * h->h_active / (dx * dx),
+                        k_ice * h->h_active / (dy * dy)};
+  const int64_t gx = (h->nx + tfg::kCondTX - 1) / tfg::kCondTX, strips = (h->ny + tfg::kCondRows - 1) / tfg::kCondRows;
+  const int64_t per_xcd = (gx * strips + 7) / 8;
+  if (8 * per_xcd > 0x7fffffff) return fail(h, TFG_ERR_ARG, "conduction: grid too large");
+  if (h->engine == TFG_F32)
+    hipLaunchKernelGGL((tfg::k_conduction<float>), (unsigned)(8 * per_xcd), tfg::kCondTX, 0, h->stream, g, K,
+                       (float*)h->qc, (int)gx, (int)strips, (int)per_xcd);
+  else
+    hipLaunchKernelGGL((tfg::k_conduction<double>), (unsigned)(8 * per_xcd), tfg::kCondTX, 0, h->stream, g, K,
+                       (double*)h->qc, (int)gx, (int)strips, (int)per_xcd);
+  HIPCHK(h, hipGetLastError());
+  // the halo rows are the caller's: finish reading them before returning
+  if (halo_north || halo_south) HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->qc_on = true;
+  return TFG_OK;
+}
+
+int tfg_conduction_off(tfg_handle* h) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  h->qc_on = false;
+  if (h->qc) {
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, hipMemsetAsync(h->qc, 0, (size_t)h->n_pad * h->rsz, h->stream));
+  }
   return TFG_OK;
 }
 

@@ -261,10 +261,13 @@ __device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st,
 // ---------------------------------------------------------------------------
 // EXACT variant (fp64, reference order)
 // ---------------------------------------------------------------------------
+// QC: add the cell's lateral conduction flux qc [W m-2] (tfg_conduction.hpp)
+// in the reference's Qc position of Q_sum (:1314); without it Qc = 0.
+template <bool QC>
 __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
                                        double P, double T_air, double Hum_sp, double P_air, double uz,
                                        int32_t q_old, int32_t& q_new, CellState& st, CellOut& o,
-                                       CellDiag& d, bool valid) {
+                                       CellDiag& d, bool valid, double qc) {
 #pragma clang fp contract(off)
   const double dt = p.dt;
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
@@ -360,8 +363,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   double LW_out = p.em_surf_sigma * pow(T_surf_K, 4.0);
   LW_out = LW_out + p.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
-  // :1314 (Qa = Qc = 0)
-  const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + 0.0;
+  // :1314 (Qa = 0; Qc = 0 unless the optional conduction term is on)
+  const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + (QC ? qc : 0.0);
   // Stull wet bulb (:1514-1520), only needed where it snows
   double T_wb = 0.0;
   if (P_snow > 0.0) {
@@ -523,10 +526,11 @@ struct CellOutF {
   float h_snow, SM, h_ice, IM, M_total, RH;
 };
 
+template <bool QC>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
                                       const tfg_uniforms& u, const double* __restrict__ geo_d, int64_t n_pad,
                                       int64_t cell, float P, float T_air, float Hum_sp, float P_air, float uz,
-                                      int32_t q_old, int32_t& q_new, CellState& st, CellOutF& o, DiagF& d) {
+                                      int32_t q_old, int32_t& q_new, CellState& st, CellOutF& o, DiagF& d, float qc) {
   const bool snow_pos = st.h_snow > 0.0, ice_pos = st.h_ice > 0.0;  // previous-step depths
   const float T_K = T_air + 273.15f;
   const float rT = frcp(T_K);
@@ -649,7 +653,8 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air, ta2 * ta2, -(ts2 * ts2));
-  const float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
+  float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
+  if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
 
   // ---- state update (:1566-1731), fp64 where depths and cold contents accumulate
   const double previous_swe = st.h_swe;

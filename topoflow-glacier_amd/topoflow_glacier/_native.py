@@ -20,7 +20,7 @@ __all__ = [
 
 LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
 
-ABI_VERSION = 3  # include/tfg.h TFG_ABI_VERSION
+ABI_VERSION = 4  # include/tfg.h TFG_ABI_VERSION
 FLOW_ALL, FLOW_INTERIOR, FLOW_EDGES = 0, 1, 2  # tfg_ice_flow_step parts
 PREV_DEPTH = -1  # tfg_get_field / tfg_set_field index: the fp64 previous-step depth (TFG_PREV_DEPTH)
 F32, F64, I32 = 0, 1, 2
@@ -31,7 +31,7 @@ FIELD = {
     "LW_in": 0, "P_air": 1, "Hum_sp": 2, "P": 3, "SW_in": 4, "T_air": 5, "uz": 6,
     "h_snow": 7, "h_swe": 8, "SM": 9, "h_ice": 10, "h_iwe": 11, "IM": 12, "M_total": 13, "RH": 14,
     "elev": 15, "slope": 16, "aspect": 17, "catch_id": 18,
-    "Eccs": 19, "Ecci": 20, "albedo": 21, "n": 22, "window": 23,
+    "Eccs": 19, "Ecci": 20, "albedo": 21, "n": 22, "window": 23, "Qc": 24,
 }
 DIAG_NAMES = ["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"]
 
@@ -118,6 +118,10 @@ def load() -> ctypes.CDLL:
         "tfg_set_inputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),
+        "tfg_conduction_edges": ([vp, dp, dp, i32], i32),
+        "tfg_conduction_update": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32],
+                                  i32),
+        "tfg_conduction_off": ([vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)
@@ -175,5 +179,5 @@ def exported_symbols() -> list[str]:
         "tfg_set_stream", "tfg_get_stream", "tfg_shared_stream", "tfg_set_field", "tfg_get_field", "tfg_init_state",
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
-        "tfg_update",
+        "tfg_update", "tfg_conduction_edges", "tfg_conduction_update", "tfg_conduction_off",
     ) if hasattr(L, n)]

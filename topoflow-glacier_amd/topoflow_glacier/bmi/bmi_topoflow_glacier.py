@@ -254,6 +254,7 @@ class BmiTopoflowGlacier(BmiBase):
         self._dirty_outputs: set[str] = set()
         self._timestep = 0
         self._flowed_at = 0
+        self._conducted_at = -1
         start = parse_time(cfg.start_time)
         self.start_year, self.start_month, self.start_day, self.start_hour = start.year, start.month, start.day, start.hour
         end = parse_time(cfg.end_time)
@@ -317,6 +318,26 @@ class BmiTopoflowGlacier(BmiBase):
             self._flowed_at = self._timestep
             self._stale = {_int(n) for n, _ in _output_vars}
 
+    def _conduct_if_due(self) -> None:
+        """The optional lateral conduction term (config ``lateral_conduction``):
+        at step k*conduction_interval (from step 0), evaluate Qc from the
+        current state; the steps of that interval add it to Q_sum (:1314).
+        Off by default (the reference's Qc = 0, :936-948)."""
+        c = self.cfg
+        if c.lateral_conduction and self._timestep % c.conduction_interval == 0 \
+                and self._conducted_at != self._timestep:
+            self._engine.conduction_update(c.k_snow, c.k_ice, c.dx, c.dy)
+            self._conducted_at = self._timestep
+
+    def _steps_to_boundary(self, k: int) -> int:
+        """k, cut where the next optional split term (ice flow, conduction) is due."""
+        c = self.cfg
+        if c.ice_flow:
+            k = min(k, c.ice_flow_interval - self._timestep % c.ice_flow_interval)
+        if c.lateral_conduction:
+            k = min(k, c.conduction_interval - self._timestep % c.conduction_interval)
+        return k
+
     def update(self) -> None:
         """Advance one time step (reference :413-465) on the GPU.  Small
         models (eager mirrors) take one synchronous tfg_update call: inputs in,
@@ -325,12 +346,14 @@ class BmiTopoflowGlacier(BmiBase):
         if not self._eager:
             self._push_inputs()
             self._flow_if_due()
+            self._conduct_if_due()
             eng.run(1)
             self._after_steps(1)
             return
         if self._dirty_outputs:
             self._push_dirty_outputs()
         self._flow_if_due()
+        self._conduct_if_due()
         block = self._in_block
         for i, v in enumerate(self._in_mirrors):
             block[i] = v
@@ -354,11 +377,10 @@ class BmiTopoflowGlacier(BmiBase):
         eng = self._require()
         self._push_inputs()
         done = 0
-        while done < n_steps:  # in chunks that end where the ice-flow term is due
+        while done < n_steps:  # in chunks that end where a split term (ice flow, conduction) is due
             self._flow_if_due()
-            k = n_steps - done
-            if self.cfg.ice_flow:
-                k = min(k, self.cfg.ice_flow_interval - self._timestep % self.cfg.ice_flow_interval)
+            self._conduct_if_due()
+            k = self._steps_to_boundary(n_steps - done)
             eng.run(k)
             self._after_steps(k)
             done += k

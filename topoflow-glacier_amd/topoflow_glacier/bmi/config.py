@@ -18,7 +18,10 @@ deliberate, additive differences:
   ``fuse_steps`` (time steps fused per kernel launch, default 24),
   ``ice_flow`` / ``ice_flow_interval`` / ``dx`` / ``dy`` (the optional
   shallow-ice flow term, off by default; it moves ice between cells every
-  ``ice_flow_interval`` steps on a grid of dx x dy metre cells).
+  ``ice_flow_interval`` steps on a grid of dx x dy metre cells) and
+  ``lateral_conduction`` / ``conduction_interval`` / ``k_snow`` / ``k_ice``
+  (the optional lateral heat-conduction term, re-evaluated every
+  ``conduction_interval`` steps).
 
 Unknown keys are ignored, as in the reference (pydantic default).
 """
@@ -118,11 +121,35 @@ class TopoflowGlacierConfig(BaseModel):
     ice_flow_interval: int = Field(24, ge=1)  # time steps between flow updates
     dx: float | None = Field(None, gt=0)      # grid spacing [m], west-east
     dy: float | None = Field(None, gt=0)      # grid spacing [m], north-south
+    # optional lateral heat conduction (extension; tfg_conduction_*): the
+    # reference's Qc (:936-948, :1314) from Fourier's law between neighbouring
+    # cells, re-evaluated every conduction_interval steps; off by default
+    lateral_conduction: bool = False
+    conduction_interval: int = Field(24, ge=1)  # time steps between Qc updates
+    k_snow: float = Field(0.1, ge=0)  # snow conductivity [W m-1 K-1] (Sturm et al. 1997 at rho_snow = 50 kg m-3)
+    k_ice: float = Field(2.1, ge=0)   # ice conductivity [W m-1 K-1] near 0 degC
 
     @model_validator(mode="after")
     def _flow_needs_spacing(self):
         if self.ice_flow and (self.dx is None or self.dy is None):
             raise ValueError("ice_flow needs the grid spacing dx and dy [m]")
+        return self
+
+    @model_validator(mode="after")
+    def _conduction_needs_spacing_and_a_stable_interval(self):
+        if not self.lateral_conduction:
+            return self
+        if self.dx is None or self.dy is None:
+            raise ValueError("lateral_conduction needs the grid spacing dx and dy [m]")
+        # Qc is held over the interval (explicit, operator-split): a cell's pack
+        # must not overshoot its neighbours, dt <= d^2/8 * rho Cp / k per layer
+        d2 = min(self.dx, self.dy) ** 2
+        limits = [d2 / 8.0 * rc / k for rc, k in ((self.rho_snow * self.Cp_snow, self.k_snow),
+                                                   (self.rho_ice * self.Cp_ice, self.k_ice)) if k > 0]
+        span = self.conduction_interval * float(self.dt) * 3600.0
+        if limits and span > min(limits):
+            raise ValueError(f"conduction_interval spans {span:.0f} s, above the stable {min(limits):.0f} s "
+                             "for this grid spacing; shorten the interval")
         return self
 
     @field_validator("start_time", "end_time", mode="before")

@@ -309,10 +309,10 @@ class GlacierEngine:
 
     # -- optional lateral ice flow (tfg_ice_flow_*, off unless called) -----------------
     @staticmethod
-    def _halo_args(north, south, nx):
+    def _halo_args(north, south, nx, rows=2):
         """Halo rows as (keep-alive, north ptr, south ptr, on_device): numpy
         arrays (host) or torch CUDA tensors (device, e.g. straight from an RCCL
-        receive), [2][nx] fp64 each, or None at the domain edge."""
+        receive), [rows][nx] fp64 each, or None at the domain edge."""
         keep, ptrs, dev = [], [], set()
         dp = ctypes.POINTER(ctypes.c_double)
         for halo in (north, south):
@@ -322,13 +322,13 @@ class GlacierEngine:
                 import torch
 
                 t = halo.reshape(-1).to(torch.float64).contiguous()
-                if t.numel() != 2 * nx:
-                    raise ValueError(f"halo rows need [2][{nx}] values")
+                if t.numel() != rows * nx:
+                    raise ValueError(f"halo rows need [{rows}][{nx}] values")
                 keep.append(t)
                 ptrs.append(ctypes.cast(ctypes.c_void_p(t.data_ptr()), dp))
                 dev.add(1)
             else:
-                a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(2, nx))
+                a = np.ascontiguousarray(np.asarray(halo, dtype=np.float64).reshape(rows, nx))
                 keep.append(a)
                 ptrs.append(a.ctypes.data_as(dp))
                 dev.add(0)
@@ -384,6 +384,38 @@ class GlacierEngine:
         from topoflow_glacier.sharding import ice_flow
 
         return ice_flow(self, dt_years, dx, dy, cfl=cfl, distributed=False)
+
+    # -- optional lateral heat conduction (tfg_conduction_*, off unless called) ------
+    def conduction_edges(self, device=None):
+        """This shard's first and last rows as conduction halo rows, [4][nx]
+        each (T_snow, h_snow, T_ice, h_ice): numpy arrays, or torch CUDA tensors
+        when `device` is given (ready for an RCCL exchange)."""
+        dp = ctypes.POINTER(ctypes.c_double)
+        if device is not None:
+            import torch
+
+            first = torch.empty((4, self.nx), dtype=torch.float64, device=device)
+            last = torch.empty((4, self.nx), dtype=torch.float64, device=device)
+            torch.cuda.current_stream(first.device).synchronize()
+            self._chk(self.lib.tfg_conduction_edges(self.h, ctypes.cast(ctypes.c_void_p(first.data_ptr()), dp),
+                                                    ctypes.cast(ctypes.c_void_p(last.data_ptr()), dp), 1))
+            return first, last  # tfg_conduction_edges synchronises the engine stream before returning
+        first, last = np.empty((4, self.nx)), np.empty((4, self.nx))
+        self._chk(self.lib.tfg_conduction_edges(self.h, first.ctypes.data_as(dp), last.ctypes.data_as(dp), 0))
+        return first, last
+
+    def conduction_update(self, k_snow: float, k_ice: float, dx: float, dy: float, north=None, south=None) -> None:
+        """Evaluate the lateral conduction flux Qc from the current state and
+        switch the term on: every later step adds Qc to Q_sum (:1314) until the
+        next update or conduction_off() (tfg_conduction_update)."""
+        keep, pn, ps, on_dev = self._halo_args(north, south, self.nx, rows=4)
+        self._chk(self.lib.tfg_conduction_update(self.h, float(k_snow), float(k_ice), float(dx), float(dy), pn, ps,
+                                                 on_dev))
+        del keep
+
+    def conduction_off(self) -> None:
+        """Qc = 0 again: the reference's energy balance (tfg_conduction_off)."""
+        self._chk(self.lib.tfg_conduction_off(self.h))
 
     # -- mass balance -------------------------------------------------------------
     def diagnostics(self) -> np.ndarray:

@@ -17,7 +17,8 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["row_block", "allreduce_diagnostics", "exchange_halo_rows", "terrain_from_dem_sharded"]
+__all__ = ["row_block", "allreduce_diagnostics", "exchange_halo_rows", "terrain_from_dem_sharded", "ice_flow",
+           "lateral_conduction"]
 
 
 def row_block(ny_global: int, rank: int, world: int) -> tuple[int, int]:
@@ -160,3 +161,30 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
         north, south = swap(first, last)
         eng.ice_flow_step(dt, dx, dy, north, south, part=FLOW_EDGES)
     return n_sub
+
+
+def lateral_conduction(eng, k_snow: float, k_ice: float, dx: float, dy: float, group=None, distributed=None) -> None:
+    """The optional lateral heat-conduction term over a row-block sharded grid
+    (tfg_conduction_*; extension): each shard swaps its
+    edge rows' pack temperatures and depths with its neighbours (one batched
+    point-to-point exchange, RCCL over xGMI on the GPU path, gloo on CPU), then
+    evaluates its Qc field, which the following steps add to Q_sum.  The
+    sharded Qc equals the unsharded one bit for bit.  `eng` is a GlacierEngine
+    (or anything with its conduction_* methods)."""
+    import torch
+    import torch.distributed as dist
+
+    on = distributed if distributed is not None else (
+        dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1)
+    if not on:
+        eng.conduction_update(k_snow, k_ice, dx, dy)
+        return
+    if dist.get_backend(group) == "nccl":  # the rows stay on the devices
+        first, last = eng.conduction_edges(device=f"cuda:{torch.cuda.current_device()}")
+        north, south = exchange_halo_rows(first.reshape(-1), last.reshape(-1), group)
+    else:
+        first, last = eng.conduction_edges()
+        north, south = exchange_halo_rows(torch.from_numpy(first.reshape(-1)), torch.from_numpy(last.reshape(-1)), group)
+        north = None if north is None else north.numpy()
+        south = None if south is None else south.numpy()
+    eng.conduction_update(k_snow, k_ice, dx, dy, north, south)
