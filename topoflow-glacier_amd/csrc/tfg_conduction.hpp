@@ -38,15 +38,14 @@
 namespace tfg {
 
 // The state planes a conduction pass reads, and the constants of the
-// temperature derivation.
+// temperature derivation.  h_swe, h_iwe, Eccs, Ecci are consecutive planes of
+// the engine state ([8][n_pad] fp64: S_HSWE .. S_ECCI), so one base pointer
+// and the plane stride n_pad address all four.
 struct CondGrid {
-  const double* swe;   // h_swe  [n]
-  const double* iwe;   // h_iwe  [n]
-  const double* eccs;  // Eccs   [n]
-  const double* ecci;  // Ecci   [n]
+  const double* st;    // h_swe plane; h_iwe, Eccs, Ecci follow at n_pad strides
   const double* hn;    // north halo [4][nx] (T_snow, h_snow, T_ice, h_ice) or null
   const double* hs;    // south halo [4][nx] or null
-  int64_t ny, nx;
+  int64_t ny, nx, n_pad;
   double ws, wi;       // rho_H2O/rho_snow, rho_H2O/rho_ice (:385-386)
   double T0;           // T0_cc (:389)
   double inv_cs;       // 1 / (rho_snow Cp_snow)
@@ -65,21 +64,47 @@ struct CondCell {
   double Ts, hs, Ti, hi;
 };
 
-__device__ __forceinline__ CondCell cond_cell(const CondGrid& g, int64_t i) {
+__device__ __forceinline__ CondCell cond_none() { return {0.0, 0.0, 0.0, 0.0}; }
+
+// (T_snow, h_snow, T_ice, h_ice) from the state values h_swe, h_iwe, Eccs, Ecci.
+__device__ __forceinline__ CondCell cond_from_state(const CondGrid& g, double swe, double iwe, double eccs,
+                                                    double ecci) {
 #pragma clang fp contract(off)
   CondCell c;
-  c.hs = g.swe[i] * g.ws;  // :1711
-  c.hi = g.iwe[i] * g.wi;  // :1726
-  c.Ts = c.hs > 0.0 ? g.T0 - (g.eccs[i] * g.inv_cs) / c.hs : g.T0;
-  c.Ti = c.hi > 0.0 ? g.T0 - g.ecci[i] * g.inv_ci : g.T0;
+  c.hs = swe * g.ws;  // :1711
+  c.hi = iwe * g.wi;  // :1726
+  c.Ts = c.hs > 0.0 ? g.T0 - (eccs * g.inv_cs) / c.hs : g.T0;
+  c.Ti = c.hi > 0.0 ? g.T0 - ecci * g.inv_ci : g.T0;
   return c;
 }
 
-__device__ __forceinline__ CondCell cond_halo(const double* row, int64_t nx, int64_t c) {
-  return {row[c], row[nx + c], row[2 * nx + c], row[3 * nx + c]};
+// One row's four values at one column as loaded: state values of an
+// in-domain row (kind 0), a halo row's cell values (kind 1), or nothing
+// beyond the domain edge (kind 2).  The loads are straight-line, from a
+// wave-uniform (base, stride) choice, so the compiler keeps them in flight
+// instead of waiting at a branch; the values are interpreted only when used.
+struct CondRaw {
+  double v[4];
+  int kind;
+};
+
+__device__ __forceinline__ CondRaw cond_fetch(const CondGrid& g, int64_t row, int64_t col) {
+  const bool in = row >= 0 && row < g.ny;
+  const double* halo = row < 0 ? g.hn : g.hs;
+  CondRaw r;
+  r.kind = in ? 0 : (halo ? 1 : 2);
+  const double* base = r.kind == 0 ? g.st + row * g.nx + col : (r.kind == 1 ? halo + col : g.st + col);
+  const int64_t stride = r.kind == 1 ? g.nx : g.n_pad;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) r.v[k] = base[k * stride];
+  return r;
 }
 
-__device__ __forceinline__ CondCell cond_none() { return {0.0, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ CondCell cond_cell(const CondGrid& g, const CondRaw& r, bool col_in) {
+  if (!col_in || r.kind == 2) return cond_none();
+  if (r.kind == 1) return {r.v[0], r.v[1], r.v[2], r.v[3]};
+  return cond_from_state(g, r.v[0], r.v[1], r.v[2], r.v[3]);
+}
 
 // One face's contribution from neighbour n to cell m (snow and ice sums).
 __device__ __forceinline__ void cond_face(const CondCell& m, const CondCell& n, double gs, double gi, double& qs,
@@ -89,40 +114,64 @@ __device__ __forceinline__ void cond_face(const CondCell& m, const CondCell& n, 
   if (m.hi > 0.0 && n.hi > 0.0) qi += (n.Ti - m.Ti) * gi;
 }
 
-constexpr int kCondTX = 256, kCondRows = 32;
+__device__ __forceinline__ void cond_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Qc of a row-block shard.  Workgroup tiles of kCondTX columns x kCondRows
-// rows; each thread walks down its column with the rows above and below in
-// registers (one new row of state per row walked) and reads its west/east
-// neighbours from the same cache lines its neighbours load.  Tiles are dealt
-// XCD-aware (the ice-flow order, tfg_flow.hpp): XCD k takes the k-th eighth
-// of the tiles in row-major order, so vertically adjacent strips share an L2.
+// Tiles of kCondTX threads over kCondOut = kCondTX - 2 output columns (one
+// overlapping column each side supplies the west/east neighbours) and
+// kCondRows rows.
+#ifndef TFG_COND_ROWS
+#define TFG_COND_ROWS 64
+#endif
+constexpr int kCondTX = 256, kCondOut = kCondTX - 2, kCondRows = TFG_COND_ROWS;
+
+// Qc of a row-block shard.  Each thread walks down one column of its tile with
+// the rows above and below in registers and the row after next already in
+// flight, so every state value crosses HBM once per tile (plus the two
+// overlap columns and the rows just above and below the strip: 1.04 x the
+// algorithmic reads at 64-row strips).  Each row's cell
+// values go through a double-buffered LDS row, one barrier per row, from which
+// a thread reads its west and east neighbours.  Tiles are dealt XCD-aware (the
+// ice-flow order, tfg_flow.hpp): XCD k takes the k-th eighth of the tiles in
+// row-major order, so vertically adjacent strips share an L2.
 template <class R>
 __global__ __launch_bounds__(kCondTX) void k_conduction(const CondGrid g, const CondK K, R* __restrict__ qc,
                                                          int gx, int strips, int per_xcd) {
 #pragma clang fp contract(off)
+  __shared__ double sC[2][4][kCondTX];
   const int64_t tile = (int64_t)(blockIdx.x % 8) * per_xcd + blockIdx.x / 8;
-  if (tile >= (int64_t)gx * strips) return;
+  if (tile >= (int64_t)gx * strips) return;  // the padding of the last eighth (whole workgroup)
+  const int t = threadIdx.x;
   const int64_t tx = tile % gx, ty = tile / gx;
-  const int64_t c = tx * kCondTX + threadIdx.x;
-  if (c >= g.nx) return;  // no barriers below
+  const int64_t c = tx * kCondOut - 1 + t;
+  const bool col_in = c >= 0 && c < g.nx;
+  const int64_t cl = col_in ? c : (c < 0 ? 0 : g.nx - 1);  // a valid address for the overlap columns
+  const bool writes = col_in && t >= 1 && t <= kCondTX - 2;
   const int64_t r0 = ty * kCondRows;
   const int64_t r1 = r0 + kCondRows < g.ny ? r0 + kCondRows : g.ny;
-  const int64_t nx = g.nx;
-  CondCell up = r0 > 0 ? cond_cell(g, (r0 - 1) * nx + c) : (g.hn ? cond_halo(g.hn, nx, c) : cond_none());
-  CondCell cur = cond_cell(g, r0 * nx + c);
+  const int tw = t > 0 ? t - 1 : 0, te = t < kCondTX - 1 ? t + 1 : t;
+  CondCell up = cond_cell(g, cond_fetch(g, r0 - 1, cl), col_in);
+  CondCell cur = cond_cell(g, cond_fetch(g, r0, cl), col_in);
+  CondRaw nxt = cond_fetch(g, r0 + 1, cl);
   for (int64_t r = r0; r < r1; ++r) {
-    const CondCell dn = r + 1 < g.ny ? cond_cell(g, (r + 1) * nx + c) : (g.hs ? cond_halo(g.hs, nx, c) : cond_none());
-    const CondCell w = c > 0 ? cond_cell(g, r * nx + c - 1) : cond_none();
-    const CondCell e = c + 1 < nx ? cond_cell(g, r * nx + c + 1) : cond_none();
+    const int b = (int)(r - r0) & 1;
+    const CondRaw ahead = cond_fetch(g, r + 2 < r1 ? r + 2 : r1, cl);  // past the strip: row r1 again (a cache hit)
+    const CondCell dn = cond_cell(g, nxt, col_in);
+    sC[b][0][t] = cur.Ts;
+    sC[b][1][t] = cur.hs;
+    sC[b][2][t] = cur.Ti;
+    sC[b][3][t] = cur.hi;
+    cond_lds_barrier();  // the row is in buffer b; buffer b^1 (row r-1) is no longer read
+    const CondCell w = {sC[b][0][tw], sC[b][1][tw], sC[b][2][tw], sC[b][3][tw]};
+    const CondCell e = {sC[b][0][te], sC[b][1][te], sC[b][2][te], sC[b][3][te]};
     double qs = 0.0, qi = 0.0;
     cond_face(cur, up, K.gsy, K.giy, qs, qi);
     cond_face(cur, dn, K.gsy, K.giy, qs, qi);
     cond_face(cur, w, K.gsx, K.gix, qs, qi);
     cond_face(cur, e, K.gsx, K.gix, qs, qi);
-    qc[r * nx + c] = (R)(qs + qi);
+    if (writes) qc[r * g.nx + c] = (R)(qs + qi);
     up = cur;
     cur = dn;
+    nxt = ahead;
   }
 }
 
@@ -130,7 +179,8 @@ __global__ __launch_bounds__(kCondTX) void k_conduction(const CondGrid g, const 
 __global__ void k_conduction_edges(const CondGrid g, double* __restrict__ first, double* __restrict__ last) {
   const int64_t nx = g.nx;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nx; c += (int64_t)gridDim.x * blockDim.x) {
-    const CondCell a = cond_cell(g, c), b = cond_cell(g, (g.ny - 1) * nx + c);
+    const CondCell a = cond_cell(g, cond_fetch(g, 0, c), true);
+    const CondCell b = cond_cell(g, cond_fetch(g, g.ny - 1, c), true);
     first[c] = a.Ts; first[nx + c] = a.hs; first[2 * nx + c] = a.Ti; first[3 * nx + c] = a.hi;
     last[c] = b.Ts; last[nx + c] = b.hs; last[2 * nx + c] = b.Ti; last[3 * nx + c] = b.hi;
   }
