@@ -499,6 +499,99 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
   }
 }
 
+// One step of a one-cell fp64 handle for tfg_update (the single-catchment BMI
+// update(), :413-465, one model per catchment as NextGen runs it): the step's
+// inputs and uniforms arrive as kernel arguments, one wave runs the step with
+// its transcendental calls batched across lanes (cell_step_exact_wave), and
+// lane 0 writes the state, the window slot, the history slot, the frame, the
+// eight outputs into the pinned host block, the diagnostic slab row and the
+// release flag.  Same arithmetic as k_fused<double, true, ...> with K = 1, so
+// the same results bit for bit; the per-launch fixed work (LDS bins, the
+// read-back of the history slot, host-memory reads of inputs and uniforms) is
+// gone from the critical path.
+struct CellIo {
+  tfg_uniforms u;
+  double in[kNumForc];  // P, T_air, Hum_sp, P_air, uz (device frame order)
+};
+
+__global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, const double* __restrict__ geo,
+                                             const int32_t* __restrict__ catch_id, double* __restrict__ st,
+                                             int64_t* __restrict__ tot, int32_t* __restrict__ ring,
+                                             double* __restrict__ forc, double* __restrict__ hist,
+                                             double* __restrict__ slab, const double* __restrict__ qcf,
+                                             int read_depths) {
+  const DevParams& p = a.p;
+  const int64_t np = a.n_pad;
+  const tfg_uniforms& u = io.u;
+  CellState cs;
+  cs.h_swe = st[S_HSWE * np];
+  cs.h_iwe = st[S_HIWE * np];
+  cs.Eccs = st[S_ECCS * np];
+  cs.Ecci = st[S_ECCI * np];
+  cs.n = st[S_N * np];
+  cs.albedo = st[S_ALB * np];
+  if (read_depths) {
+    cs.h_snow = st[S_HSNOW * np];
+    cs.h_ice = st[S_HICE * np];
+  } else {
+    cs.h_snow = cs.h_swe * p.ws;  // :1711, bit-identical to the last step
+    cs.h_ice = cs.h_iwe * p.wi;   // :1726
+  }
+  cs.tot_q = tot[0];
+  const int32_t q_old = ring[(int64_t)u.slot * np];
+  const CellStatic sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
+  double* srow = slab + (catch_id ? catch_id[0] : 0) * 6;
+  double sv[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sv[i] = srow[i];
+  const double qc = qcf ? qcf[0] : 0.0;
+  CellDiag d;
+  diag_zero(d);
+  CellOut o;
+  int32_t q_new;
+  tfg::cell_step_exact_wave(p, sx, u, io.in[F_P], io.in[F_T], io.in[F_Q], io.in[F_PA], io.in[F_UZ], q_old, q_new, cs, o,
+                            d, qc);
+  if (threadIdx.x == 0) {
+    ring[(int64_t)u.slot * np] = q_new;
+    double* h = hist + (int64_t)u.hist * kNumHist * np;
+    h[H_HSNOW * np] = o.h_snow;
+    h[H_SM * np] = o.SM;
+    h[H_HICE * np] = o.h_ice;
+    h[H_IM * np] = o.IM;
+    h[H_MTOT * np] = o.M_total;
+    h[H_RH * np] = o.RH;
+    double* fr = forc + (int64_t)u.frame * kNumForc * np;
+#pragma unroll
+    for (int f = 0; f < kNumForc; ++f) fr[f * np] = io.in[f];
+    st[S_HSWE * np] = cs.h_swe;
+    st[S_HIWE * np] = cs.h_iwe;
+    st[S_ECCS * np] = cs.Eccs;
+    st[S_ECCI * np] = cs.Ecci;
+    st[S_N * np] = cs.n;
+    st[S_ALB * np] = cs.albedo;
+    tot[0] = cs.tot_q;
+    double* out = a.io_out;  // [8][1]: h_snow, h_swe, SM, h_ice, h_iwe, IM, M_total, RH
+    out[0] = o.h_snow;
+    out[1] = cs.h_swe;
+    out[2] = o.SM;
+    out[3] = o.h_ice;
+    out[4] = cs.h_iwe;
+    out[5] = o.IM;
+    out[6] = o.M_total;
+    out[7] = o.RH;
+    // the slab row as k_fused accumulates it (wave and workgroup sums of one
+    // cell add zeros)
+    srow[0] = sv[0] + d.P;
+    srow[1] = sv[1] + d.PR;
+    srow[2] = sv[2] + d.PS;
+    srow[3] = sv[3] + d.SM;
+    srow[4] = sv[4] + d.IM;
+    srow[5] = tfg::npmax(sv[5], d.Pmax);
+    __threadfence_system();
+    __hip_atomic_store(a.io_flag, a.io_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Per-cell solar geometry of the fast engine, once per static-raster change:
 // kGeoF fp32 planes then [tan(eq_lat), t_noon] fp64 (tfg::derive_geo).
 template <class R>
@@ -1385,15 +1478,14 @@ int fused_blocks(const tfg_handle* h) {
   return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
 }
 
-int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
-                 const IoArgs& io = IoArgs()) {
+// Work a launch of the step kernels depends on: window totals after slots were
+// set, and the per-cell geometry after the static rasters changed.
+int prepare_steps(tfg_handle* h) {
   if (h->tot_dirty) {  // window slots were set: rebuild the running totals
     hipLaunchKernelGGL(k_window_total, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->ring, h->ring_len, h->n_pad);
     HIPCHK(h, hipGetLastError());
     h->tot_dirty = false;
   }
-  const int blocks = fused_blocks(h);
-  const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
   if (h->geo_dirty) {
     if (h->engine == TFG_F32)
       hipLaunchKernelGGL((k_prepare_geo<float>), grid_for(h->n_pad), 256, 0, h->stream, h->dp, (const float*)h->stat,
@@ -1404,6 +1496,14 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
     HIPCHK(h, hipGetLastError());
     h->geo_dirty = false;
   }
+  return TFG_OK;
+}
+
+int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
+                 const IoArgs& io = IoArgs()) {
+  if (int rc = prepare_steps(h)) return rc;
+  const int blocks = fused_blocks(h);
+  const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
   const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
@@ -1620,6 +1720,25 @@ extern "C" void tfg_update_timing(double* out) {
 #define TFG_TACC(i, a, b)
 #endif
 
+namespace {
+// Wait for the workgroups' release flags of a tfg_update launch (a few
+// microseconds sooner than a stream synchronisation); after ~2 ms fall back to
+// the stream wait, which also reports a failed launch.
+int wait_flags(tfg_handle* h, size_t flag_off, int blocks, uint32_t seq) {
+  const volatile uint32_t* fl = reinterpret_cast<const volatile uint32_t*>(h->io_h + flag_off);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool done = false;
+  for (int64_t spins = 0; !done; ++spins) {
+    done = true;
+    for (int b = 0; b < blocks && done; ++b) done = fl[b] == seq;
+    if (!done && (spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+  }
+  if (done) std::atomic_thread_fence(std::memory_order_acquire);
+  else HIPCHK(h, hipStreamSynchronize(h->stream));
+  return TFG_OK;
+}
+}  // namespace
+
 int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
                int dst_dtype, int64_t n) {
   TFG_TSTAMP(t_in0);
@@ -1655,6 +1774,47 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
   }
   // BMI order (P_air, Hum_sp, P, T_air, uz) -> frame fields, converted to the engine type
   static const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};
+  if (h->engine == TFG_F64 && n == 1) {
+    // one catchment (NextGen's per-catchment model): k_cell, inputs and
+    // uniforms as kernel arguments, one wave
+    CellIo cio;
+    cio.u = *u;
+    for (int f = 0; f < 5; ++f)
+      cio.in[map[f]] = src_dtype == TFG_F64 ? static_cast<const double*>(src)[f] : (double)static_cast<const float*>(src)[f];
+    KArgs a;
+    a.p = h->dp;
+    a.K = 1;
+    a.n_catch = h->n_catch;
+    a.n = h->n;
+    a.n_pad = h->n_pad;
+    a.io_in = nullptr;
+    a.io_out = reinterpret_cast<double*>(h->io_d + out_off);
+    a.io_flag = reinterpret_cast<uint32_t*>(h->io_d + flag_off);
+    a.io_seq = ++h->io_seq == 0 ? ++h->io_seq : h->io_seq;  // never 0, the initial flag value
+    TFG_TSTAMP(t_c0);
+    TFG_TACC(0, t_in0, t_c0);
+    if (int rc = prepare_steps(h)) return rc;
+    hipLaunchKernelGGL(k_cell, 1, 64, 0, h->stream, a, cio, reinterpret_cast<const double*>(h->geo), h->catch_id,
+                       h->st, h->tot, h->ring, static_cast<double*>(h->forc), static_cast<double*>(h->hist), h->slab,
+                       h->qc_on ? static_cast<const double*>(h->qc) : nullptr, h->depths_derived ? 0 : 1);
+    HIPCHK(h, hipGetLastError());
+    h->depths_derived = true;
+    h->last_hist = u->hist;
+    TFG_TSTAMP(t_c1);
+    TFG_TACC(1, t_c0, t_c1);
+    if (int rc = wait_flags(h, flag_off, 1, a.io_seq)) return rc;
+    TFG_TSTAMP(t_c2);
+    TFG_TACC(2, t_c1, t_c2);
+    const double* oh = reinterpret_cast<const double*>(h->io_h + out_off);
+    if (dst_dtype == TFG_F64) std::memcpy(dst, oh, out_b);
+    else for (int64_t i = 0; i < 8; ++i) static_cast<float*>(dst)[i] = (float)oh[i];
+    TFG_TSTAMP(t_c3);
+    TFG_TACC(3, t_c2, t_c3);
+#ifdef TFG_UPDATE_TIMING
+    g_upd_ns[4] += 1;
+#endif
+    return TFG_OK;
+  }
   for (int f = 0; f < 5; ++f) {
     char* o = h->io_h + (size_t)map[f] * np * h->rsz;
     if (src_dtype == TFG_F64) {
@@ -1678,21 +1838,7 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
   if (int rc = launch_steps(h, reinterpret_cast<const tfg_uniforms*>(h->io_d + u_off), u, 1, io)) return rc;
   TFG_TSTAMP(t_l1);
   TFG_TACC(1, t_in1, t_l1);
-  // Wait for the workgroups' release flags (a few microseconds sooner than a
-  // stream synchronisation); after ~2 ms fall back to the stream wait, which
-  // also reports a failed launch.
-  {
-    const volatile uint32_t* fl = reinterpret_cast<const volatile uint32_t*>(h->io_h + flag_off);
-    const auto t0 = std::chrono::steady_clock::now();
-    bool done = false;
-    for (int64_t spins = 0; !done; ++spins) {
-      done = true;
-      for (int b = 0; b < blocks && done; ++b) done = fl[b] == io.seq;
-      if (!done && (spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
-    }
-    if (done) std::atomic_thread_fence(std::memory_order_acquire);
-    else HIPCHK(h, hipStreamSynchronize(h->stream));
-  }
+  if (int rc = wait_flags(h, flag_off, blocks, io.seq)) return rc;
   TFG_TSTAMP(t_w1);
   TFG_TACC(2, t_l1, t_w1);
   const double* oh = reinterpret_cast<const double*>(h->io_h + out_off);
@@ -1891,14 +2037,14 @@ int cond_setup(tfg_handle* h, const double* hn, const double* hs, int on_dev, tf
   const hipMemcpyKind k = on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
   if (hn) HIPCHK(h, hipMemcpyAsync(h->cond_halo, hn, (size_t)4 * nx * 8, k, h->stream));
   if (hs) HIPCHK(h, hipMemcpyAsync(h->cond_halo + 4 * nx, hs, (size_t)4 * nx * 8, k, h->stream));
-  g.swe = h->st + S_HSWE * np;
-  g.iwe = h->st + S_HIWE * np;
-  g.eccs = h->st + S_ECCS * np;
-  g.ecci = h->st + S_ECCI * np;
+  static_assert(S_HIWE == S_HSWE + 1 && S_ECCS == S_HSWE + 2 && S_ECCI == S_HSWE + 3,
+                "k_conduction reads h_swe, h_iwe, Eccs, Ecci as consecutive planes");
+  g.st = h->st + S_HSWE * np;
   g.hn = hn ? h->cond_halo : nullptr;
   g.hs = hs ? h->cond_halo + 4 * nx : nullptr;
   g.ny = h->ny;
   g.nx = nx;
+  g.n_pad = np;
   g.ws = h->dp.ws;
   g.wi = h->dp.wi;
   g.T0 = h->dp.T0;
@@ -1935,7 +2081,7 @@ int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx,
   if (int rc = ensure_qc(h)) return rc;
   const tfg::CondK K = {k_snow / (dx * dx), k_snow / (dy * dy), k_ice * h->h_active / (dx * dx),
                         k_ice * h->h_active / (dy * dy)};
-  const int64_t gx = (h->nx + tfg::kCondTX - 1) / tfg::kCondTX, strips = (h->ny + tfg::kCondRows - 1) / tfg::kCondRows;
+  const int64_t gx = (h->nx + tfg::kCondOut - 1) / tfg::kCondOut, strips = (h->ny + tfg::kCondRows - 1) / tfg::kCondRows;
   const int64_t per_xcd = (gx * strips + 7) / 8;
   if (8 * per_xcd > 0x7fffffff) return fail(h, TFG_ERR_ARG, "conduction: grid too large");
   if (h->engine == TFG_F32)

@@ -247,6 +247,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
 
 // Albedo ageing (:1020-1059) given the window predicate (exact variant).
 __device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st, bool wet_window, double T_air) {
+#pragma clang fp contract(off)  // 0.4 + 0.44 * exp(...) rounds the product first, as numpy does
   // n: where(tot >= .03, 0, n); where(tot < .03, n + days_per_dt, n)
   st.n = wet_window ? 0.0 : st.n + p.days_per_dt;
   const double r = (T_air > 0.0) ? 0.12 : 0.05;
@@ -256,6 +257,18 @@ __device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st,
   if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
   st.albedo = albedo;
   return albedo;
+}
+
+// A value the compiler cannot see as a constant.  pow() calls with a constant
+// exponent (T^4, RH^1.5) or base (10^y) go through it, so that the compiler
+// emits the general pow in every kernel: the library's call-simplification
+// may otherwise rewrite pow(x, 4.0) as multiplications in one kernel and not
+// in another, and the one-cell step (cell_step_exact_wave, whose exponents are
+// per-lane values) would no longer equal the grid step bit for bit.  numpy's
+// `** 4.0` is the general pow too.
+__device__ __forceinline__ double opaque(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -290,7 +303,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (!p.satterlund) {
     e_sat_air = 0.611 * exp((17.3 * T_air) / (T_air + 237.3));
   } else {
-    e_sat_air = pow(10.0, 11.4 - 2353.0 / (T_air + 273.15)) / 1000.0;
+    e_sat_air = pow(opaque(10.0), 11.4 - 2353.0 / (T_air + 273.15)) / 1000.0;
   }
   e_sat_air = e_sat_air * 10.0;
   // :817-826
@@ -307,7 +320,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (!p.satterlund) {
     e_sat_surf = 0.611 * exp((17.3 * T_surf) / (T_surf + 237.3));
   } else {
-    e_sat_surf = pow(10.0, 11.4 - 2353.0 / (T_surf + 273.15)) / 1000.0;
+    e_sat_surf = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15)) / 1000.0;
   }
   e_sat_surf = e_sat_surf * 10.0;
   // :640-644, per cell
@@ -359,8 +372,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
-  const double LW_in = em_air * p.sigma * pow(T_air_K, 4.0);
-  double LW_out = p.em_surf_sigma * pow(T_surf_K, 4.0);
+  const double LW_in = em_air * p.sigma * pow(T_air_K, opaque(4.0));
+  double LW_out = p.em_surf_sigma * pow(T_surf_K, opaque(4.0));
   LW_out = LW_out + p.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
   // :1314 (Qa = 0; Qc = 0 unless the optional conduction term is on)
@@ -369,9 +382,170 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   double T_wb = 0.0;
   if (P_snow > 0.0) {
     T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
-           ((0.00391838 * pow(RH, 1.5)) * atan(0.023101 * RH)) - 4.86035;
+           ((0.00391838 * pow(RH, opaque(1.5))) * atan(0.023101 * RH)) - 4.86035;
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
+#if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
+  { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_ET, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// EXACT variant for ONE cell on a whole wave (the single-catchment BMI step,
+// k_cell): every lane computes the same scalar arithmetic as cell_step_exact,
+// in the same order, but the transcendental calls are batched by dependency
+// level -- each level's calls of one function run once, lane i evaluating the
+// i-th argument -- and the results are read back from their lanes.  One wave
+// runs the step either way; batching cuts the serial chain of fp64 libm
+// calls from 14-22 (exp x7, log x2, pow x3-4, cos, acos, atan x4 where it
+// snows) to 9 (exp, log, pow, cos, acos | exp, pow, atan | exp).  The same
+// functions on the same arguments give the same values, so the result equals
+// cell_step_exact bit for bit (tests: update() through k_cell against
+// update_until() through k_fused).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double lane_value(double v, int l) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
+                                            double P, double T_air, double Hum_sp, double P_air, double uz,
+                                            int32_t q_old, int32_t& q_new, CellState& st, CellOut& o,
+                                            CellDiag& d, double qc) {
+#pragma clang fp contract(off)
+  const int lane = (int)(threadIdx.x & 63);
+  const double dt = p.dt;
+  const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
+  const double T_K = T_air + 273.15;
+  // :567, :576, :585, :604, :613, :623
+  const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
+  const double P_snow = P * ((T_air <= p.T_rs) ? 1.0 : 0.0);
+  d.P += P * p.da_m2 * dt;
+  d.Pmax = npmax(d.Pmax, P);
+  d.PR += P_rain * p.da_m2 * dt;
+  d.PS += P_snow * p.da_m2 * dt;
+  // :817-826
+  double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
+  e = e / 1000.0;
+  const double e_air = e * 10.0;
+  const double T_air_K = T_air + 273.15;
+  // window and days since snowfall (:1023-1040), ahead of the albedo exp
+  q_new = window_q(P_snow * dt * p.ws, p.qscale);
+  st.tot_q += (int64_t)q_new - (int64_t)q_old;
+  st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
+  const double r_alb = (T_air > 0.0) ? 0.12 : 0.05;
+
+  // ---- level 1: arguments from inputs, state, statics and uniforms
+  const double x_p0 = p.negM_g * s.elev / (p.R * T_K);        // :551
+  const double x_es = (17.3 * T_air) / (T_air + 237.3);        // :788
+  const double x_alb = -st.n * r_alb;                          // :1041
+  const double ex1 = exp(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
+  const double lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : e_air / 6.1121);  // :670, :888
+  const double cos_wl = cos(u.omega_th + s.dlon);               // SF:867 (same argument in every lane)
+  const double ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325
+  double px, py;
+  if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167), T_a^4 (:1231)
+    px = lane == 1 ? T_air_K : (e_air / 10.0) / T_air_K;
+    py = lane == 1 ? 4.0 : p.one_seventh;
+  } else {              // e_air^(T/2016) (:1190), T_a^4, 10^(...) of e_sat_air (:796)
+    px = lane == 1 ? T_air_K : (lane == 2 ? 10.0 : e_air);
+    py = lane == 1 ? 4.0 : (lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
+  }
+  const double pw1 = pow(px, py);
+  const double e_p0 = lane_value(ex1, 0), e_es = lane_value(ex1, 1), e_alb = lane_value(ex1, 2);
+  const double log_term = lane_value(lg1, 0), log_dn = lane_value(lg1, 1);
+  const double pw_em = lane_value(pw1, 0), pw_ta4 = lane_value(pw1, 1), pw_es = lane_value(pw1, 2);
+
+  // :551-556
+  double p0 = p.sea_p0 * e_p0;
+  p0 = p0 / 1000.0;
+  p0 = p0 * 10.0;
+  // :788-802, :838
+  double e_sat_air = !p.satterlund ? 0.611 * e_es : pw_es / 1000.0;
+  e_sat_air = e_sat_air * 10.0;
+  const double RH = e_air / e_sat_air;
+  // :888-893, :906-910
+  const double T_dew = 257.14 * log_term / (18.678 - log_term);
+  const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
+  // :640-644, :670-726, :744-745
+  const double top = p.gz * (T_air - T_surf);
+  double bot = (uz * uz) * (T_air + 273.15);
+  if (bot == 0.0) bot = 0.01;
+  const double Ri = top / bot;
+  const double arg = p.kappa / log_dn;
+  const double Dn = uz * (arg * arg);
+  const double Dh = (Ri > 0.0) ? Dn / (1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
+  // albedo (:1041-1059)
+  const double snow_albedo = 0.4 + 0.44 * e_alb;
+  double albedo = (st.h_snow > 0.0) ? snow_albedo : st.albedo;
+  if (st.h_snow == 0.0 && st.h_ice > 0.0) albedo = 0.3;
+  if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
+  st.albedo = albedo;
+  // sunrise / sunset on the slope (SF:783-830)
+  const double T_sr = npmax(-1.0 * ac / p.omega + s.t_noon, u.flat_sr);
+  const double T_ss = npmin(ac / p.omega + s.t_noon, u.flat_ss);
+  const double T_surf_K = T_surf + 273.15;
+
+  // ---- level 2: after T_dew, T_surf and RH
+  double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
+  if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
+  const double ex2 = exp(ea2);
+  double qx = lane == 1 ? RH : T_surf_K, qy = lane == 1 ? 1.5 : 4.0;             // :1520, :1233
+  if (p.satterlund && lane == 2) { qx = 10.0; qy = 11.4 - 2353.0 / (T_surf + 273.15); }  // :796 (surface)
+  const double pw2 = pow(qx, qy);
+  double at2 = 0.0;
+  if (P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
+    at2 = atan(lane == 1 ? T_air + RH : (lane == 2 ? RH - 1.676331 : (lane == 3 ? 0.023101 * RH
+                                                                                 : 0.151977 * sqrt(RH + 8.313659))));
+  double e_sat_surf = !p.satterlund ? 0.611 * lane_value(ex2, 0) : lane_value(pw2, 2) / 1000.0;
+  e_sat_surf = e_sat_surf * 10.0;
+  const double W_p = 1.12 * lane_value(ex2, 1);
+  // :853, :931-934
+  const double e_surf = RH * e_sat_surf;
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
+  const double a_sa = -0.1240 - (0.0207 * W_p);
+  const double b_sa = -0.0682 - (0.0248 * W_p);
+  const double a_s = -0.0363 - (0.0084 * W_p);
+  const double b_s = -0.0572 - (0.0173 * W_p);
+
+  // ---- level 3: after W_p
+  const double ex3 = exp(lane == 1 ? a_s + (b_s * u.m_opt) : a_sa + (b_sa * u.m_opt));  // SF:610, SF:652
+  const double tau = npmin(npmax(lane_value(ex3, 0) - p.dust, 0.0), 1.0);
+  double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos_wl + s.sin_leq * u.sin_d);
+  K_ET = npmax(K_ET, 0.0);
+  const double gam_s = (1.0 - lane_value(ex3, 1)) + p.dust;
+  const double K_dif = 0.5 * gam_s * u.k_et_flat;
+  const double K_global = tau * u.k_et_flat + K_dif;
+  const double K_bs = 0.5 * gam_s * albedo * K_global;
+  double K_cs = (tau * K_ET) + K_dif + K_bs;
+  if ((u.th <= T_sr) || (u.th >= T_ss)) K_cs = 0.0;
+  const double Qn_SW = K_cs * (1.0 - albedo);  // :1139
+  // :1167-1192, :1231-1248
+  double em_air;
+  if (!p.satterlund) {
+    const double term1 = p.one_minus_F_172 * pw_em;
+    em_air = (term1 * p.cloud_term) + p.F;
+  } else {
+    em_air = 1.08 * (1.0 - lane_value(ex2, 2));
+  }
+  const double LW_in = em_air * p.sigma * pw_ta4;
+  double LW_out = p.em_surf_sigma * lane_value(pw2, 0);
+  LW_out = LW_out + p.one_minus_em_surf * LW_in;
+  const double Qn_LW = LW_in - LW_out;
+  // :1314 (Qa = 0; qc = 0 unless the optional conduction term is on)
+  const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + qc;
+  double T_wb = 0.0;
+  if (P_snow > 0.0) {
+    T_wb = T_air * lane_value(at2, 0) + lane_value(at2, 1) - lane_value(at2, 2) +
+           ((0.00391838 * lane_value(pw2, 1)) * lane_value(at2, 3)) - 4.86035;
+  }
+  melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
+#if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
+  { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_ET, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
+#endif
 }
 
 // ---------------------------------------------------------------------------
