@@ -523,6 +523,9 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
   const DevParams& p = a.p;
   const int64_t np = a.n_pad;
   const tfg_uniforms& u = io.u;
+#ifdef TFG_CELL_TIMING  // diagnostic build: phase times [wall-clock ticks] replace the outputs
+  const long long tt0 = wall_clock64();
+#endif
   CellState cs;
   cs.h_swe = st[S_HSWE * np];
   cs.h_iwe = st[S_HIWE * np];
@@ -549,8 +552,17 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
   diag_zero(d);
   CellOut o;
   int32_t q_new;
+#ifdef TFG_CELL_TIMING
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  asm volatile("" ::"v"(cs.h_swe), "v"(sx.elev), "v"(sv[0]), "v"(q_old));
+  const long long tt1 = wall_clock64();
+#endif
   tfg::cell_step_exact_wave(p, sx, u, io.in[F_P], io.in[F_T], io.in[F_Q], io.in[F_PA], io.in[F_UZ], q_old, q_new, cs, o,
                             d, qc);
+#ifdef TFG_CELL_TIMING
+  asm volatile("" ::"v"(o.SM), "v"(o.RH), "v"(cs.Eccs), "v"(o.h_snow), "v"(d.SM));
+  const long long tt2 = wall_clock64();
+#endif
   if (threadIdx.x == 0) {
     ring[(int64_t)u.slot * np] = q_new;
     double* h = hist + (int64_t)u.hist * kNumHist * np;
@@ -587,6 +599,13 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
     srow[3] = sv[3] + d.SM;
     srow[4] = sv[4] + d.IM;
     srow[5] = tfg::npmax(sv[5], d.Pmax);
+#ifdef TFG_CELL_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const long long tt3 = wall_clock64();
+    out[0] = (double)(tt1 - tt0);
+    out[1] = (double)(tt2 - tt1);
+    out[2] = (double)(tt3 - tt2);
+#endif
     __threadfence_system();
     __hip_atomic_store(a.io_flag, a.io_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
