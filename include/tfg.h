@@ -343,9 +343,12 @@ int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n
  * blocking). */
 int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_device);
 /* Evaluate Qc from the current state and switch the term on (k_snow, k_ice
- * [W m-1 K-1], dx, dy [m]); the halo rows are read before the call returns. */
-int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, const double* halo_north,
-                          const double* halo_south, int halo_on_device);
+ * [W m-1 K-1], dx, dy [m]; q_ground [W m-2] is added to every cell: the
+ * ground heat flux, the reference's declared but unused geothermal flux Qg,
+ * config.py:84 / :333, converted from J yr-1 m-2; 0 for none).  The halo rows
+ * are read before the call returns. */
+int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, double q_ground,
+                          const double* halo_north, const double* halo_south, int halo_on_device);
 /* Switch the term off (Qc = 0: the reference's energy balance again). */
 int tfg_conduction_off(tfg_handle* h);
 

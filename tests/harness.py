@@ -588,7 +588,7 @@ def conduction_cells(swe, iwe, eccs, ecci, cfg: dict):
 
 
 def conduction_restated(swe, iwe, eccs, ecci, cfg: dict, k_snow: float, k_ice: float, dx: float, dy: float,
-                        north=None, south=None):
+                        north=None, south=None, q_ground: float = 0.0):
     """Qc [W m-2] of a [ny][nx] shard; north/south halo rows [4][nx] (T_snow,
     h_snow, T_ice, h_ice) or None at the domain edge (no flux)."""
     c = dict(O.CFG_DEFAULTS)
@@ -614,7 +614,7 @@ def conduction_restated(swe, iwe, eccs, ecci, cfg: dict, k_snow: float, k_ice: f
         qs = np.where(ms, qs + (np.minimum(hs, nhs) * (nTs - Ts)) * gs, qs)
         mi = (hi > 0) & (nhi > 0)
         qi = np.where(mi, qi + (nTi - Ti) * gi, qi)
-    return qs + qi
+    return (qs + qi) + q_ground
 
 
 class RestatedCondShard:
@@ -631,8 +631,8 @@ class RestatedCondShard:
         cells = conduction_cells(*self.state, self.cfg)
         return np.stack([a[0] for a in cells]), np.stack([a[-1] for a in cells])
 
-    def conduction_update(self, k_snow, k_ice, dx, dy, north=None, south=None):
-        self.qc = conduction_restated(*self.state, self.cfg, k_snow, k_ice, dx, dy, north, south)
+    def conduction_update(self, k_snow, k_ice, dx, dy, north=None, south=None, q_ground=0.0):
+        self.qc = conduction_restated(*self.state, self.cfg, k_snow, k_ice, dx, dy, north, south, q_ground)
 
 
 def conduction_state(ny: int, nx: int, seed: int = 3):

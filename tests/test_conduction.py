@@ -259,3 +259,63 @@ def test_bmi_conduction_every_interval(tmp_path):
     np.testing.assert_array_equal(res[0][1], res[1][1])
     assert np.abs(res[0][1]).max() > 0.0 and np.all(res[2][1] == 0.0)
     assert np.abs(res[0][0] - res[2][0]).max() > 0.0
+
+
+# ------------------------------------------------------ ground heat flux (Qg)
+QG = 1575000.0 / (3600.0 * 24 * 365)  # config.py:84 default [J yr-1 m-2] -> W m-2 (:283, :333)
+
+
+def test_restated_ground_flux_adds_to_every_cell():
+    st = conduction_state(7, 9)
+    base = conduction_restated(*st, CFG, KS, KI, DX, DY)
+    np.testing.assert_array_equal(conduction_restated(*st, CFG, KS, KI, DX, DY, q_ground=QG), base + QG)
+    from tests.harness import cfg_object
+
+    assert cfg_object(CFG).ground_heat_flux is False and cfg_object(dict(CFG, ground_heat_flux=True)).ground_heat_flux
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["float32", "float64"])
+def test_gpu_conduction_with_ground_flux_matches_restatement(engine):
+    full = conduction_state(35, 70)
+    e = _engine(full, engine)
+    try:
+        e.conduction_update(KS, KI, DX, DY, q_ground=QG)
+        want = conduction_restated(*full, CFG, KS, KI, DX, DY, q_ground=QG)
+        np.testing.assert_array_equal(e.get_field("Qc").reshape(35, 70), _as_engine(want, engine))
+    finally:
+        e.close()
+
+
+@pytest.mark.gpu
+def test_bmi_ground_heat_flux_matches_the_oracle(tmp_path):
+    """ground_heat_flux: true on the reference's single-catchment workflow
+    (one-cell BMI, k_cell): every step adds Qg (config.py:84, :333) to Q_sum
+    (:1314); the outputs equal the oracle run with Qc = Qg / sec_per_year to
+    1e-10, and differ from the run without it."""
+    import yaml
+
+    from tests.harness import GOLDEN, O, load_golden
+    from topoflow_glacier.run import run_catchment
+
+    g = load_golden("cat3062920_265")
+    res = {}
+    for on in (True, False):
+        path = tmp_path / f"cat_{on}.yaml"
+        path.write_text(yaml.dump(dict(BASE_CFG, ground_heat_flux=on)))
+        res[on] = run_catchment(path, forcing=GOLDEN / "sample-cat-3062920.csv", mode="bmi")
+    cfg = dict(g["cfg"])
+    m = O.OracleGrid(cfg, **g["static"])
+    m.Qc = np.float64(QG)
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], g["nsteps"], cfg["lon"], g["tz_name"])
+    ref = {k: [] for k in ("h_snow", "SM", "M_total", "RH")}
+    for k in range(g["nsteps"]):
+        r = m.step(*(g["forcing"][n][k] for n in ("P", "T_air", "Hum_sp", "P_air", "uz")), jd[k], tsn[k])
+        for v in ref:
+            ref[v].append(float(r[v][0]))
+    for v, want in ref.items():
+        want = np.array(want)
+        got = np.asarray(res[True][v], np.float64)
+        err = np.abs(got - want) / np.maximum(np.abs(want), 1e-300)
+        assert np.all(np.where(want != 0, err, np.abs(got)) <= 1e-10), v
+    assert np.abs(np.asarray(res[True]["SM"]) - np.asarray(res[False]["SM"])).max() > 0.0

@@ -21,7 +21,9 @@
 //   ice:  k_ice * h_active_layer * (T_ice_j - T_ice_i) / d^2
 //         when both cells hold ice;
 // no flux across the domain edge.  Qc_i sums the snow faces (north, south,
-// west, east) and the ice faces, in that order, in fp64.  The two cells of a
+// west, east) and the ice faces, in that order, in fp64, then adds the
+// optional ground heat flux: the reference's declared but unused geothermal
+// flux Qg (config.py:84, :333) in W m-2.  The two cells of a
 // face evaluate the same products of the same values, so their fluxes are
 // exact negatives of each other and the domain total is zero up to the
 // rounding of the per-cell sums.
@@ -57,6 +59,7 @@ struct CondGrid {
 struct CondK {
   double gsx, gsy;  // k_snow / dx^2, k_snow / dy^2
   double gix, giy;  // k_ice h_active_layer / dx^2, k_ice h_active_layer / dy^2
+  double qg;        // ground (geothermal) heat flux [W m-2] added to every cell
 };
 
 // A cell as its neighbours see it; an absent neighbour has no snow and no ice.
@@ -168,7 +171,7 @@ __global__ __launch_bounds__(kCondTX) void k_conduction(const CondGrid g, const 
     cond_face(cur, dn, K.gsy, K.giy, qs, qi);
     cond_face(cur, w, K.gsx, K.gix, qs, qi);
     cond_face(cur, e, K.gsx, K.gix, qs, qi);
-    if (writes) qc[r * g.nx + c] = (R)(qs + qi);
+    if (writes) qc[r * g.nx + c] = (R)((qs + qi) + K.qg);
     up = cur;
     cur = dn;
     nxt = ahead;

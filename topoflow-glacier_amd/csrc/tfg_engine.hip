@@ -2089,8 +2089,8 @@ int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_devi
   return TFG_OK;
 }
 
-int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, const double* halo_north,
-                          const double* halo_south, int halo_on_device) {
+int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, double q_ground,
+                          const double* halo_north, const double* halo_south, int halo_on_device) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
   if (!(k_snow >= 0) || !(k_ice >= 0)) return fail(h, TFG_ERR_ARG, "conductivities must be >= 0");
@@ -2098,8 +2098,9 @@ int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx,
   tfg::CondGrid g;
   if (int rc = cond_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
   if (int rc = ensure_qc(h)) return rc;
+  if (!std::isfinite(q_ground)) return fail(h, TFG_ERR_ARG, "ground heat flux must be finite");
   const tfg::CondK K = {k_snow / (dx * dx), k_snow / (dy * dy), k_ice * h->h_active / (dx * dx),
-                        k_ice * h->h_active / (dy * dy)};
+                        k_ice * h->h_active / (dy * dy), q_ground};
   const int64_t gx = (h->nx + tfg::kCondOut - 1) / tfg::kCondOut, strips = (h->ny + tfg::kCondRows - 1) / tfg::kCondRows;
   const int64_t per_xcd = (gx * strips + 7) / 8;
   if (8 * per_xcd > 0x7fffffff) return fail(h, TFG_ERR_ARG, "conduction: grid too large");

@@ -119,8 +119,8 @@ def load() -> ctypes.CDLL:
         "tfg_get_outputs": ([vp, i32, vp, i32, i64, i32], i32),
         "tfg_update": ([vp, i32, vp, i32, vp, vp, i32, i64], i32),
         "tfg_conduction_edges": ([vp, dp, dp, i32], i32),
-        "tfg_conduction_update": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, dp, dp, i32],
-                                  i32),
+        "tfg_conduction_update": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                   ctypes.c_double, dp, dp, i32], i32),
         "tfg_conduction_off": ([vp], i32),
     }
     for name, (args, res) in sigs.items():

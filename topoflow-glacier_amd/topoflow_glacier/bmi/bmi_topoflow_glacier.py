@@ -248,6 +248,10 @@ class BmiTopoflowGlacier(BmiBase):
         self._out_mirrors = [self._outputs.value(name) for name, _ in _output_vars]
         self._engine = make_engine(cfg)
         self._beta_invalid = configure_engine(self._engine, cfg)
+        # the optional ground heat flux: Qg (:333) in W m-2, held in Qc
+        self._q_ground = float(cfg.geothermal_heat_flux) / float(self.sec_per_year) if cfg.ground_heat_flux else 0.0
+        if cfg.ground_heat_flux and not cfg.lateral_conduction:
+            self._engine.set_field("Qc", np.float64(self._q_ground))
         for name, key in (("h_snow", "h0_snow"), ("h_ice", "h0_ice"), ("h_swe", "h0_swe"), ("h_iwe", "h0_iwe")):
             self._outputs.set_value(_ext(name), np.float64(getattr(cfg, key)))
         self._stale.clear()
@@ -326,7 +330,7 @@ class BmiTopoflowGlacier(BmiBase):
         c = self.cfg
         if c.lateral_conduction and self._timestep % c.conduction_interval == 0 \
                 and self._conducted_at != self._timestep:
-            self._engine.conduction_update(c.k_snow, c.k_ice, c.dx, c.dy)
+            self._engine.conduction_update(c.k_snow, c.k_ice, c.dx, c.dy, q_ground=self._q_ground)
             self._conducted_at = self._timestep
 
     def _steps_to_boundary(self, k: int) -> int:

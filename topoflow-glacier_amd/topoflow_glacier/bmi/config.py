@@ -21,7 +21,8 @@ deliberate, additive differences:
   ``ice_flow_interval`` steps on a grid of dx x dy metre cells) and
   ``lateral_conduction`` / ``conduction_interval`` / ``k_snow`` / ``k_ice``
   (the optional lateral heat-conduction term, re-evaluated every
-  ``conduction_interval`` steps).
+  ``conduction_interval`` steps) and ``ground_heat_flux`` (adds the declared
+  ``geothermal_heat_flux`` to every cell's conduction flux).
 
 Unknown keys are ignored, as in the reference (pydantic default).
 """
@@ -128,6 +129,9 @@ class TopoflowGlacierConfig(BaseModel):
     conduction_interval: int = Field(24, ge=1)  # time steps between Qc updates
     k_snow: float = Field(0.1, ge=0)  # snow conductivity [W m-1 K-1] (Sturm et al. 1997 at rho_snow = 50 kg m-3)
     k_ice: float = Field(2.1, ge=0)   # ice conductivity [W m-1 K-1] near 0 degC
+    # optional ground heat flux: the declared but unused geothermal flux Qg
+    # (geothermal_heat_flux [J yr-1 m-2], reference :333) added to every cell's Qc
+    ground_heat_flux: bool = False
 
     @model_validator(mode="after")
     def _flow_needs_spacing(self):

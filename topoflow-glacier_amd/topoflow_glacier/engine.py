@@ -404,13 +404,15 @@ class GlacierEngine:
         self._chk(self.lib.tfg_conduction_edges(self.h, first.ctypes.data_as(dp), last.ctypes.data_as(dp), 0))
         return first, last
 
-    def conduction_update(self, k_snow: float, k_ice: float, dx: float, dy: float, north=None, south=None) -> None:
-        """Evaluate the lateral conduction flux Qc from the current state and
-        switch the term on: every later step adds Qc to Q_sum (:1314) until the
-        next update or conduction_off() (tfg_conduction_update)."""
+    def conduction_update(self, k_snow: float, k_ice: float, dx: float, dy: float, north=None, south=None,
+                          q_ground: float = 0.0) -> None:
+        """Evaluate the lateral conduction flux Qc from the current state (plus
+        a uniform ground heat flux q_ground [W m-2]) and switch the term on:
+        every later step adds Qc to Q_sum (:1314) until the next update or
+        conduction_off() (tfg_conduction_update)."""
         keep, pn, ps, on_dev = self._halo_args(north, south, self.nx, rows=4)
-        self._chk(self.lib.tfg_conduction_update(self.h, float(k_snow), float(k_ice), float(dx), float(dy), pn, ps,
-                                                 on_dev))
+        self._chk(self.lib.tfg_conduction_update(self.h, float(k_snow), float(k_ice), float(dx), float(dy),
+                                                 float(q_ground), pn, ps, on_dev))
         del keep
 
     def conduction_off(self) -> None:

@@ -163,7 +163,8 @@ def ice_flow(eng, dt_years: float, dx: float, dy: float, cfl: float = 0.5, group
     return n_sub
 
 
-def lateral_conduction(eng, k_snow: float, k_ice: float, dx: float, dy: float, group=None, distributed=None) -> None:
+def lateral_conduction(eng, k_snow: float, k_ice: float, dx: float, dy: float, group=None, distributed=None,
+                       q_ground: float = 0.0) -> None:
     """The optional lateral heat-conduction term over a row-block sharded grid
     (tfg_conduction_*; extension): each shard swaps its
     edge rows' pack temperatures and depths with its neighbours (one batched
@@ -177,7 +178,7 @@ def lateral_conduction(eng, k_snow: float, k_ice: float, dx: float, dy: float, g
     on = distributed if distributed is not None else (
         dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1)
     if not on:
-        eng.conduction_update(k_snow, k_ice, dx, dy)
+        eng.conduction_update(k_snow, k_ice, dx, dy, q_ground=q_ground)
         return
     if dist.get_backend(group) == "nccl":  # the rows stay on the devices
         first, last = eng.conduction_edges(device=f"cuda:{torch.cuda.current_device()}")
@@ -187,4 +188,4 @@ def lateral_conduction(eng, k_snow: float, k_ice: float, dx: float, dy: float, g
         north, south = exchange_halo_rows(torch.from_numpy(first.reshape(-1)), torch.from_numpy(last.reshape(-1)), group)
         north = None if north is None else north.numpy()
         south = None if south is None else south.numpy()
-    eng.conduction_update(k_snow, k_ice, dx, dy, north, south)
+    eng.conduction_update(k_snow, k_ice, dx, dy, north, south, q_ground=q_ground)
