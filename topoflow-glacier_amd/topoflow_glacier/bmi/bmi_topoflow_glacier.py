@@ -241,11 +241,21 @@ class BmiTopoflowGlacier(BmiBase):
                           ("land_surface__aspect_angle", "aspect")):
             self._static.set_value(name, np.float64(getattr(cfg, key)))
         self._eager = n <= _EAGER_MAX_CELLS
-        self._in_block = np.empty((5, n), dtype=np.float64)
-        self._out_block = np.empty((8, n), dtype=np.float64)
-        # the mirrors are updated in place (Context.set_value), so resolve them once
-        self._in_mirrors = [self._dynamic_inputs.value(_ext(name)) for name in _INPUT_BLOCK]
-        self._out_mirrors = [self._outputs.value(name) for name, _ in _output_vars]
+        # The five physics inputs and the eight outputs are rows of one block
+        # each, in tfg_set_inputs / tfg_get_outputs order: the engine reads the
+        # inputs and writes the outputs in one transfer, with no copies between
+        # the blocks and the BMI variables (set_value copies into the rows,
+        # get_value_ptr hands them out).
+        self._in_block = np.zeros((5, n), dtype=np.float64)
+        self._out_block = np.zeros((8, n), dtype=np.float64)
+        for i, name in enumerate(_INPUT_BLOCK):
+            self._dynamic_inputs.bind(_ext(name), self._in_block[i])
+        for j, (name, _) in enumerate(_output_vars):
+            self._outputs.bind(name, self._out_block[j])
+        # name -> (host array, internal output name or None): the per-call lookup
+        # of set_value / get_value (NextGen makes 15 of them per catchment-step)
+        self._arrays = {v.name: (v.value, None) for c in (self._static, self._dynamic_inputs) for v in c}
+        self._arrays.update({v.name: (v.value, _int(v.name)) for v in self._outputs})
         self._engine = make_engine(cfg)
         self._beta_invalid = configure_engine(self._engine, cfg)
         # the optional ground heat flux: Qg (:333) in W m-2, held in Qc
@@ -276,12 +286,7 @@ class BmiTopoflowGlacier(BmiBase):
         return self._engine
 
     def _push_inputs(self) -> None:
-        eng = self._engine
-        n = self.n_cells
-        block = self._in_block
-        for i, name in enumerate(_INPUT_BLOCK):  # one transfer for the five inputs (tfg_set_inputs)
-            block[i] = np.broadcast_to(self._dynamic_inputs.value(_ext(name)), (n,))
-        eng.set_inputs(block, 0)
+        self._engine.set_inputs(self._in_block, 0)  # one transfer for the five inputs (tfg_set_inputs)
         self._push_dirty_outputs()
 
     def _push_dirty_outputs(self) -> None:
@@ -358,13 +363,8 @@ class BmiTopoflowGlacier(BmiBase):
             self._push_dirty_outputs()
         self._flow_if_due()
         self._conduct_if_due()
-        block = self._in_block
-        for i, v in enumerate(self._in_mirrors):
-            block[i] = v
-        out = eng.update_io(block, self._out_block)
+        eng.update_io(self._in_block, self._out_block)  # the outputs land in the BMI variables
         self._timestep += 1
-        for dst, row in zip(self._out_mirrors, out):
-            dst[:] = row
         self._stale.clear()
 
     def update_until(self, time: float) -> None:
@@ -400,9 +400,7 @@ class BmiTopoflowGlacier(BmiBase):
     # ------------------------------------------------------------- mirrors
     def _refresh_all(self) -> None:
         """All eight outputs in one gather + copy (tfg_get_outputs)."""
-        out = self._engine.get_outputs(out=self._out_block)
-        for j, (name, _) in enumerate(_output_vars):
-            self._outputs.value(name)[:] = out[j]
+        self._engine.get_outputs(out=self._out_block)  # the block's rows are the BMI variables
         self._stale.clear()
 
     def _refresh(self, internal: str) -> None:
@@ -411,6 +409,12 @@ class BmiTopoflowGlacier(BmiBase):
         self._stale.discard(internal)
 
     def _mirror(self, external: str) -> np.ndarray:
+        hit = getattr(self, "_arrays", {}).get(external)
+        if hit is not None:
+            internal = hit[1]
+            if internal is not None and self._engine is not None and internal in self._stale:
+                self._refresh(internal)
+            return hit[0]
         ctx = first_containing(external, self._outputs, self._dynamic_inputs, self._static)
         if ctx is self._outputs and self._engine is not None:
             internal = _int(external)
@@ -453,10 +457,15 @@ class BmiTopoflowGlacier(BmiBase):
             self._static.set_value(name, src)
             self._set_static(name)
             return
-        ctx = first_containing(name, self._outputs, self._dynamic_inputs, self._static)
-        ctx.set_value(name, src)
-        if ctx is self._outputs:
-            internal = _int(name)
+        hit = getattr(self, "_arrays", {}).get(name)
+        if hit is None:  # before initialize(), or an unknown name (KeyError)
+            ctx = first_containing(name, self._outputs, self._dynamic_inputs, self._static)
+            ctx.set_value(name, src)
+            hit = (None, _int(name) if ctx is self._outputs else None)
+        else:
+            hit[0][:] = src
+        internal = hit[1]
+        if internal is not None:
             self._stale.discard(internal)
             self._dirty_outputs.add(internal)
 
@@ -475,7 +484,7 @@ class BmiTopoflowGlacier(BmiBase):
         """Copy of a variable, flattened into `dest` (reference :1810-1824)."""
         value = self.get_value_ptr(name)
         try:
-            dest[:] = value.flatten()
+            dest[:] = value.reshape(-1)
         except Exception as e:
             raise RuntimeError(f"Could not return value {name} as flattened array") from e
         return dest

@@ -41,6 +41,12 @@ class Context:
     def set_value(self, name: str, value) -> None:
         self._vars[name].value[:] = value
 
+    def bind(self, name: str, array: np.ndarray) -> None:
+        """Back a variable by `array` (e.g. one row of a block the engine fills
+        in one transfer), keeping its current values."""
+        array[:] = self._vars[name].value
+        self._vars[name].value = array
+
     def set_value_at_indices(self, name: str, inds: np.ndarray, src: np.ndarray) -> None:
         if src.shape[0] < inds.shape[0]:
             raise ValueError("inds larger than src")
