@@ -319,3 +319,18 @@ def test_bmi_ground_heat_flux_matches_the_oracle(tmp_path):
         err = np.abs(got - want) / np.maximum(np.abs(want), 1e-300)
         assert np.all(np.where(want != 0, err, np.abs(got)) <= 1e-10), v
     assert np.abs(np.asarray(res[True]["SM"]) - np.asarray(res[False]["SM"])).max() > 0.0
+
+
+@pytest.mark.gpu
+def test_gpu_coupled_conduction_over_a_year():
+    """A year (8760 hourly steps) of the coupled term on 1 m cells, Qc
+    re-evaluated every 24 steps from each side's own state: the fp64 engine
+    matches the oracle run the same way at 1e-10 every step, with the flip
+    rule (the coupling adds no drift).  The fp32 engine's year-long behaviour
+    is characterised by test_gpu_parity.py::test_fp32_free_run_over_a_year
+    (compared once a day; melt onsets, where E_in - Eccs cancels, are many in
+    a year of melt and are not a per-step 1e-5 quantity)."""
+    ny, nx, nsteps = 8, 8, 8760
+    cond = dict(k_snow=KS, k_ice=KI, dx=1.0, dy=1.0, every=24)
+    r = run_gpu_vs_oracle(ny, nx, nsteps, engine="float64", seed=23, cold=_cold(ny, nx, 8), conduction=cond)
+    assert r["ok"], r["summary"]
