@@ -18,7 +18,7 @@ REPS = 40
 if len(sys.argv) > 2 and sys.argv[1] == "--summary":
     rows = []
     for f in glob.glob(f"{sys.argv[2]}/**/*kernel_trace.csv", recursive=True):
-        rows += [r for r in csv.DictReader(open(f)) if "k_fused<double, true" in r["Kernel_Name"]]
+        rows += [r for r in csv.DictReader(open(f)) if "k_fused<double, true" in r["Kernel_Name"] or "k_cell_run" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows]
     d = d[len(d) - len(KS) * REPS:]  # the timed launches (the warm-up ones come first)

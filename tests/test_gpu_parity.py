@@ -246,6 +246,47 @@ def test_fusion_is_invisible(engine):
         assert np.array_equal(a[1][v], b[1][v]) and np.array_equal(a[1][v], c[1][v]), v
 
 
+@pytest.mark.gpu
+def test_one_cell_kernels_equal_the_grid_kernel():
+    """A one-cell fp64 handle runs k_cell (tfg_update, the BMI's update()) or
+    k_cell_run (tfg_step: update_until, bulk runs), which batch the step's
+    transcendental calls across the wave's lanes; a grid runs
+    k_fused<double, true, ...> with one cell per lane.  Same arithmetic, same
+    bits: cells of the grid64 fixture run both ways over 100 steps."""
+    from tests.harness import make_engine
+
+    g = load_golden("grid64")
+    nsteps = 100
+    grid = gpu_run_fields(g["cfg"], g["static"], g["forcing"], 8, 8, "float64", nsteps, fuse_steps=24)
+    order = ("P_air", "Hum_sp", "P", "T_air", "uz")  # tfg_update / update_io input order
+    for c in (0, 17, 42, 63):
+        static = {k: v[c:c + 1] for k, v in g["static"].items()}
+        forcing = {k: v[:, c:c + 1] for k, v in g["forcing"].items()}
+        run = gpu_run_fields(g["cfg"], static, forcing, 1, 1, "float64", nsteps, fuse_steps=24)
+        e = make_engine(g["cfg"], 1, 1, "float64", n_frames=1, hist_depth=1)
+        try:
+            for k in ("elev", "slope", "aspect"):
+                e.set_field(k, static[k])
+            for k in ("h_snow", "h_ice", "h_swe", "h_iwe"):
+                e.set_field(k, static["h0_" + k[2:]])
+            e.init_state()
+            out = np.empty((8, 1))
+            upd = {v: [] for v in HIST}
+            for k in range(nsteps):
+                e.update_io(np.array([[forcing[n][k, 0]] for n in order], dtype=np.float64), out)
+                for j, v in enumerate(("h_snow", "h_swe", "SM", "h_ice", "h_iwe", "IM", "M_total", "RH")):
+                    if v in upd:
+                        upd[v].append(out[j, 0])
+            state = {v: e.get_field(v) for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")}
+        finally:
+            e.close()
+        for v in HIST:
+            assert np.array_equal(run[0][v][:, 0], grid[0][v][:, c]), (c, v, "k_cell_run")
+            assert np.array_equal(np.array(upd[v]), grid[0][v][:, c]), (c, v, "k_cell")
+        for v in state:
+            assert run[1][v][0] == grid[1][v][c] == state[v][0], (c, v)
+
+
 @pytest.mark.parametrize("fuse,chunks,n_catch", [(96, None, 1), (100, None, 1), (150, None, 1), (192, [192, 58], 1),
                                                   (96, [1, 96, 96, 57], 1), (150, None, 200)])
 def test_launches_longer_than_the_window_are_invisible(fuse, chunks, n_catch):

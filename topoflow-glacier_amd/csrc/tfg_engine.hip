@@ -611,6 +611,89 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
   }
 }
 
+// K consecutive steps of a one-cell fp64 handle (tfg_step: update_until and
+// bulk runs of one catchment): k_cell's lane-batched step in a loop, the state
+// in registers, each step's frame values, window slot and uniforms requested
+// one step ahead (a one-slot window runs one step per launch, tfg_step).
+// Same arithmetic as k_fused<double, true, ...>, so the same results bit for
+// bit.  Every lane stores the same values to the same addresses, so no store
+// sits behind a branch.
+__global__ __launch_bounds__(64) void k_cell_run(const KArgs a, const tfg_uniforms* __restrict__ uni,
+                                                 const double* __restrict__ geo, const int32_t* __restrict__ catch_id,
+                                                 double* __restrict__ st, int64_t* __restrict__ tot,
+                                                 int32_t* __restrict__ ring, const double* __restrict__ forc,
+                                                 double* __restrict__ hist, double* __restrict__ slab,
+                                                 const double* __restrict__ qcf, int read_depths) {
+  const DevParams& p = a.p;
+  const int64_t np = a.n_pad;
+  CellState cs;
+  cs.h_swe = st[S_HSWE * np];
+  cs.h_iwe = st[S_HIWE * np];
+  cs.Eccs = st[S_ECCS * np];
+  cs.Ecci = st[S_ECCI * np];
+  cs.n = st[S_N * np];
+  cs.albedo = st[S_ALB * np];
+  if (read_depths) {
+    cs.h_snow = st[S_HSNOW * np];
+    cs.h_ice = st[S_HICE * np];
+  } else {
+    cs.h_snow = cs.h_swe * p.ws;  // :1711, bit-identical to the last step
+    cs.h_ice = cs.h_iwe * p.wi;   // :1726
+  }
+  cs.tot_q = tot[0];
+  const CellStatic sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
+  double* srow = slab + (catch_id ? catch_id[0] : 0) * 6;
+  double sv[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sv[i] = srow[i];
+  const double qc = qcf ? qcf[0] : 0.0;
+  CellDiag d;
+  diag_zero(d);
+  struct In {
+    double v[kNumForc];
+    int32_t q;
+  };
+  auto fetch = [&](int k, In& x) {
+    const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
+    const double* fr = forc + (int64_t)un->frame * kNumForc * np;
+#pragma unroll
+    for (int f = 0; f < kNumForc; ++f) x.v[f] = fr[f * np];
+    x.q = ring[(int64_t)un->slot * np];
+  };
+  In cur, nxt;
+  fetch(0, cur);
+  for (int k = 0; k < a.K; ++k) {
+    fetch(k + 1, nxt);
+    const tfg_uniforms u = uni[k];
+    CellOut o;
+    int32_t q_new;
+    tfg::cell_step_exact_wave(p, sx, u, cur.v[F_P], cur.v[F_T], cur.v[F_Q], cur.v[F_PA], cur.v[F_UZ], cur.q, q_new, cs,
+                              o, d, qc);
+    ring[(int64_t)u.slot * np] = q_new;
+    double* h = hist + (int64_t)u.hist * kNumHist * np;
+    h[H_HSNOW * np] = o.h_snow;
+    h[H_SM * np] = o.SM;
+    h[H_HICE * np] = o.h_ice;
+    h[H_IM * np] = o.IM;
+    h[H_MTOT * np] = o.M_total;
+    h[H_RH * np] = o.RH;
+    cur = nxt;
+  }
+  st[S_HSWE * np] = cs.h_swe;
+  st[S_HIWE * np] = cs.h_iwe;
+  st[S_ECCS * np] = cs.Eccs;
+  st[S_ECCI * np] = cs.Ecci;
+  st[S_N * np] = cs.n;
+  st[S_ALB * np] = cs.albedo;
+  tot[0] = cs.tot_q;
+  srow[0] = sv[0] + d.P;  // the slab row as k_fused accumulates it
+  srow[1] = sv[1] + d.PR;
+  srow[2] = sv[2] + d.PS;
+  srow[3] = sv[3] + d.SM;
+  srow[4] = sv[4] + d.IM;
+  srow[5] = tfg::npmax(sv[5], d.Pmax);
+}
+
 // Per-cell solar geometry of the fast engine, once per static-raster change:
 // kGeoF fp32 planes then [tan(eq_lat), t_noon] fp64 (tfg::derive_geo).
 template <class R>
@@ -1524,10 +1607,30 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   const int blocks = fused_blocks(h);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
   const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
+  const bool one_cell = h->engine == TFG_F64 && h->n == 1 && !io.in;  // k_cell_run
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
-    int rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io)
-                                    : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io);
+    int rc = TFG_OK;
+    if (one_cell) {
+      KArgs a;
+      a.p = h->dp;
+      a.K = K;
+      a.n_catch = h->n_catch;
+      a.n = h->n;
+      a.n_pad = h->n_pad;
+      a.io_in = nullptr;
+      a.io_out = nullptr;
+      a.io_flag = nullptr;
+      a.io_seq = 0;
+      hipLaunchKernelGGL(k_cell_run, 1, 64, 0, h->stream, a, d_u + k0, reinterpret_cast<const double*>(h->geo),
+                         h->catch_id, h->st, h->tot, h->ring, static_cast<const double*>(h->forc),
+                         static_cast<double*>(h->hist), h->slab, h->qc_on ? static_cast<const double*>(h->qc) : nullptr,
+                         h->depths_derived ? 0 : 1);
+      HIPCHK(h, hipGetLastError());
+    } else {
+      rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io)
+                                  : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io);
+    }
     if (rc) return rc;
     h->depths_derived = true;
   }
