@@ -501,9 +501,10 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
 
 // One step of a one-cell fp64 handle for tfg_update (the single-catchment BMI
 // update(), :413-465, one model per catchment as NextGen runs it): the step's
-// inputs and uniforms arrive as kernel arguments, one wave runs the step with
-// its transcendental calls batched across lanes (cell_step_exact_wave), and
-// lane 0 writes the state, the window slot, the history slot, the frame, the
+// inputs and uniforms arrive as kernel arguments, one workgroup of four waves
+// (one per SIMD) runs the step with its transcendental calls batched across
+// lanes and function classes across waves (cell_step_exact_wave), and
+// thread 0 writes the state, the window slot, the history slot, the frame, the
 // eight outputs into the pinned host block, the diagnostic slab row and the
 // release flag.  Same arithmetic as k_fused<double, true, ...> with K = 1, so
 // the same results bit for bit; the per-launch fixed work (LDS bins, the
@@ -514,12 +515,13 @@ struct CellIo {
   double in[kNumForc];  // P, T_air, Hum_sp, P_air, uz (device frame order)
 };
 
-__global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, const double* __restrict__ geo,
+__global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, const CellIo io, const double* __restrict__ geo,
                                              const int32_t* __restrict__ catch_id, double* __restrict__ st,
                                              int64_t* __restrict__ tot, int32_t* __restrict__ ring,
                                              double* __restrict__ forc, double* __restrict__ hist,
                                              double* __restrict__ slab, const double* __restrict__ qcf,
                                              int read_depths) {
+  __shared__ double lds_x[tfg::X_SLOTS * 4];
   const DevParams& p = a.p;
   const int64_t np = a.n_pad;
   const tfg_uniforms& u = io.u;
@@ -557,8 +559,8 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
   asm volatile("" ::"v"(cs.h_swe), "v"(sx.elev), "v"(sv[0]), "v"(q_old));
   const long long tt1 = wall_clock64();
 #endif
-  tfg::cell_step_exact_wave(p, sx, u, io.in[F_P], io.in[F_T], io.in[F_Q], io.in[F_PA], io.in[F_UZ], q_old, q_new, cs, o,
-                            d, qc);
+  tfg::cell_step_exact_wave<tfg::kCellWaves>(p, sx, u, io.in[F_P], io.in[F_T], io.in[F_Q], io.in[F_PA], io.in[F_UZ],
+                                              q_old, q_new, cs, o, d, qc, lds_x);
 #ifdef TFG_CELL_TIMING
   asm volatile("" ::"v"(o.SM), "v"(o.RH), "v"(cs.Eccs), "v"(o.h_snow), "v"(d.SM));
   const long long tt2 = wall_clock64();
@@ -616,14 +618,16 @@ __global__ __launch_bounds__(64) void k_cell(const KArgs a, const CellIo io, con
 // in registers, each step's frame values, window slot and uniforms requested
 // one step ahead (a one-slot window runs one step per launch, tfg_step).
 // Same arithmetic as k_fused<double, true, ...>, so the same results bit for
-// bit.  Every lane stores the same values to the same addresses, so no store
-// sits behind a branch.
-__global__ __launch_bounds__(64) void k_cell_run(const KArgs a, const tfg_uniforms* __restrict__ uni,
+// bit.  Every thread stores the same values to the same addresses, so no
+// store sits behind a branch and each wave reads back only window slots it
+// wrote itself.
+__global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell_run(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                  const double* __restrict__ geo, const int32_t* __restrict__ catch_id,
                                                  double* __restrict__ st, int64_t* __restrict__ tot,
                                                  int32_t* __restrict__ ring, const double* __restrict__ forc,
                                                  double* __restrict__ hist, double* __restrict__ slab,
                                                  const double* __restrict__ qcf, int read_depths) {
+  __shared__ double lds_x[tfg::X_SLOTS * 4];
   const DevParams& p = a.p;
   const int64_t np = a.n_pad;
   CellState cs;
@@ -667,8 +671,8 @@ __global__ __launch_bounds__(64) void k_cell_run(const KArgs a, const tfg_unifor
     const tfg_uniforms u = uni[k];
     CellOut o;
     int32_t q_new;
-    tfg::cell_step_exact_wave(p, sx, u, cur.v[F_P], cur.v[F_T], cur.v[F_Q], cur.v[F_PA], cur.v[F_UZ], cur.q, q_new, cs,
-                              o, d, qc);
+    tfg::cell_step_exact_wave<tfg::kCellWaves>(p, sx, u, cur.v[F_P], cur.v[F_T], cur.v[F_Q], cur.v[F_PA], cur.v[F_UZ],
+                                                cur.q, q_new, cs, o, d, qc, lds_x);
     ring[(int64_t)u.slot * np] = q_new;
     double* h = hist + (int64_t)u.hist * kNumHist * np;
     h[H_HSNOW * np] = o.h_snow;
@@ -1622,7 +1626,7 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
       a.io_out = nullptr;
       a.io_flag = nullptr;
       a.io_seq = 0;
-      hipLaunchKernelGGL(k_cell_run, 1, 64, 0, h->stream, a, d_u + k0, reinterpret_cast<const double*>(h->geo),
+      hipLaunchKernelGGL(k_cell_run, 1, 64 * tfg::kCellWaves, 0, h->stream, a, d_u + k0, reinterpret_cast<const double*>(h->geo),
                          h->catch_id, h->st, h->tot, h->ring, static_cast<const double*>(h->forc),
                          static_cast<double*>(h->hist), h->slab, h->qc_on ? static_cast<const double*>(h->qc) : nullptr,
                          h->depths_derived ? 0 : 1);
@@ -1898,7 +1902,7 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
   static const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};
   if (h->engine == TFG_F64 && n == 1) {
     // one catchment (NextGen's per-catchment model): k_cell, inputs and
-    // uniforms as kernel arguments, one wave
+    // uniforms as kernel arguments, one workgroup of four waves
     CellIo cio;
     cio.u = *u;
     for (int f = 0; f < 5; ++f)
@@ -1916,7 +1920,7 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
     TFG_TSTAMP(t_c0);
     TFG_TACC(0, t_in0, t_c0);
     if (int rc = prepare_steps(h)) return rc;
-    hipLaunchKernelGGL(k_cell, 1, 64, 0, h->stream, a, cio, reinterpret_cast<const double*>(h->geo), h->catch_id,
+    hipLaunchKernelGGL(k_cell, 1, 64 * tfg::kCellWaves, 0, h->stream, a, cio, reinterpret_cast<const double*>(h->geo), h->catch_id,
                        h->st, h->tot, h->ring, static_cast<double*>(h->forc), static_cast<double*>(h->hist), h->slab,
                        h->qc_on ? static_cast<const double*>(h->qc) : nullptr, h->depths_derived ? 0 : 1);
     HIPCHK(h, hipGetLastError());

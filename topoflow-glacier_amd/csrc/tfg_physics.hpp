@@ -391,17 +391,20 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
 }
 
 // ---------------------------------------------------------------------------
-// EXACT variant for ONE cell on a whole wave (the single-catchment BMI step,
-// k_cell): every lane computes the same scalar arithmetic as cell_step_exact,
-// in the same order, but the transcendental calls are batched by dependency
-// level -- each level's calls of one function run once, lane i evaluating the
-// i-th argument -- and the results are read back from their lanes.  One wave
-// runs the step either way; batching cuts the serial chain of fp64 libm
-// calls from 14-22 (exp x7, log x2, pow x3-4, cos, acos, atan x4 where it
-// snows) to 9 (exp, log, pow, cos, acos | exp, pow, atan | exp).  The same
+// EXACT variant for ONE cell on a whole workgroup (the single-catchment BMI
+// step, k_cell / k_cell_run).  Every lane of every wave computes the same
+// scalar arithmetic as cell_step_exact, in the same order, but the
+// transcendental calls are batched by dependency level: each level's calls of
+// one function run once, lane i evaluating the i-th argument.  With W = 4
+// waves (one per SIMD of the CU), the function classes of a level also run
+// side by side, wave c taking class c (level 1: pow | exp | log | cos, acos;
+// level 2: pow | exp | atan; level 3: exp), and their results meet in LDS
+// behind one barrier per level; with W = 1 the classes run one after another
+// in the wave and the results are read back from their lanes (v_readlane).
+// The serial chain of fp64 libm calls falls from 14-22 (exp x7, log x2,
+// pow x3-4, cos, acos, atan x4 where it snows) to 3 levels.  The same
 // functions on the same arguments give the same values, so the result equals
-// cell_step_exact bit for bit (tests: update() through k_cell against
-// update_until() through k_fused).
+// cell_step_exact bit for bit (test_one_cell_kernels_equal_the_grid_kernel).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double lane_value(double v, int l) {
   const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -410,12 +413,34 @@ __device__ __forceinline__ double lane_value(double v, int l) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Class slots of the level exchange: [slot][4 lanes] doubles in LDS.
+enum { X_POW1 = 0, X_EXP1, X_LOG1, X_TRIG1, X_POW2, X_EXP2, X_ATAN2, X_EXP3, X_SLOTS };
+constexpr int kCellWaves = 4;
+
+// Results of one function class: computed by wave `owner` (all waves when
+// W = 1), read by every wave.
+template <int W>
+struct LevelXchg {
+  double* x;   // [X_SLOTS][4] in LDS (W > 1)
+  int wave;    // this wave's index (wave-uniform)
+  int lane;
+  __device__ bool mine(int slot) const { return W == 1 || wave == slot % W; }
+  __device__ void put(int slot, double v) const {
+    if (W > 1 && wave == slot % W && lane < 4) x[slot * 4 + lane] = v;
+  }
+  __device__ double get(int slot, double v, int l) const { return W == 1 ? lane_value(v, l) : x[slot * 4 + l]; }
+};
+
+__device__ __forceinline__ void lds_level_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int W>
 __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
                                             double P, double T_air, double Hum_sp, double P_air, double uz,
                                             int32_t q_old, int32_t& q_new, CellState& st, CellOut& o,
-                                            CellDiag& d, double qc) {
+                                            CellDiag& d, double qc, double* lds_x) {
 #pragma clang fp contract(off)
   const int lane = (int)(threadIdx.x & 63);
+  const LevelXchg<W> X{lds_x, W == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane};
   const double dt = p.dt;
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
   const double T_K = T_air + 273.15;
@@ -438,25 +463,41 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double r_alb = (T_air > 0.0) ? 0.12 : 0.05;
 
   // ---- level 1: arguments from inputs, state, statics and uniforms
-  const double x_p0 = p.negM_g * s.elev / (p.R * T_K);        // :551
-  const double x_es = (17.3 * T_air) / (T_air + 237.3);        // :788
-  const double x_alb = -st.n * r_alb;                          // :1041
-  const double ex1 = exp(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
-  const double lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : e_air / 6.1121);  // :670, :888
-  const double cos_wl = cos(u.omega_th + s.dlon);               // SF:867 (same argument in every lane)
-  const double ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325
-  double px, py;
-  if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167), T_a^4 (:1231)
-    px = lane == 1 ? T_air_K : (e_air / 10.0) / T_air_K;
-    py = lane == 1 ? 4.0 : p.one_seventh;
-  } else {              // e_air^(T/2016) (:1190), T_a^4, 10^(...) of e_sat_air (:796)
-    px = lane == 1 ? T_air_K : (lane == 2 ? 10.0 : e_air);
-    py = lane == 1 ? 4.0 : (lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
+  double ex1 = 0.0, lg1 = 0.0, cos_wl = 0.0, ac = 0.0, pw1 = 0.0;
+  if (X.mine(X_EXP1)) {
+    const double x_p0 = p.negM_g * s.elev / (p.R * T_K);        // :551
+    const double x_es = (17.3 * T_air) / (T_air + 237.3);        // :788
+    const double x_alb = -st.n * r_alb;                          // :1041
+    ex1 = exp(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
-  const double pw1 = pow(px, py);
-  const double e_p0 = lane_value(ex1, 0), e_es = lane_value(ex1, 1), e_alb = lane_value(ex1, 2);
-  const double log_term = lane_value(lg1, 0), log_dn = lane_value(lg1, 1);
-  const double pw_em = lane_value(pw1, 0), pw_ta4 = lane_value(pw1, 1), pw_es = lane_value(pw1, 2);
+  if (X.mine(X_LOG1)) lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : e_air / 6.1121);  // :670, :888
+  if (X.mine(X_TRIG1)) {
+    cos_wl = cos(u.omega_th + s.dlon);                                        // SF:867 (one argument)
+    ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));            // SF:325 (one argument)
+  }
+  if (X.mine(X_POW1)) {
+    double px, py;
+    if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167), T_a^4 (:1231)
+      px = lane == 1 ? T_air_K : (e_air / 10.0) / T_air_K;
+      py = lane == 1 ? 4.0 : p.one_seventh;
+    } else {              // e_air^(T/2016) (:1190), T_a^4, 10^(...) of e_sat_air (:796)
+      px = lane == 1 ? T_air_K : (lane == 2 ? 10.0 : e_air);
+      py = lane == 1 ? 4.0 : (lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
+    }
+    pw1 = pow(px, py);
+  }
+  X.put(X_EXP1, ex1);
+  X.put(X_LOG1, lg1);
+  X.put(X_TRIG1, lane == 1 ? ac : cos_wl);
+  X.put(X_POW1, pw1);
+  if (W > 1) lds_level_barrier();
+  const double e_p0 = X.get(X_EXP1, ex1, 0), e_es = X.get(X_EXP1, ex1, 1), e_alb = X.get(X_EXP1, ex1, 2);
+  const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1);
+  const double pw_em = X.get(X_POW1, pw1, 0), pw_ta4 = X.get(X_POW1, pw1, 1), pw_es = X.get(X_POW1, pw1, 2);
+  if (W > 1) {
+    cos_wl = X.get(X_TRIG1, 0.0, 0);
+    ac = X.get(X_TRIG1, 0.0, 1);
+  }
 
   // :551-556
   double p0 = p.sea_p0 * e_p0;
@@ -490,19 +531,27 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double T_surf_K = T_surf + 273.15;
 
   // ---- level 2: after T_dew, T_surf and RH
-  double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
-  if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
-  const double ex2 = exp(ea2);
-  double qx = lane == 1 ? RH : T_surf_K, qy = lane == 1 ? 1.5 : 4.0;             // :1520, :1233
-  if (p.satterlund && lane == 2) { qx = 10.0; qy = 11.4 - 2353.0 / (T_surf + 273.15); }  // :796 (surface)
-  const double pw2 = pow(qx, qy);
-  double at2 = 0.0;
-  if (P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
+  double ex2 = 0.0, pw2 = 0.0, at2 = 0.0;
+  if (X.mine(X_EXP2)) {
+    double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
+    if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
+    ex2 = exp(ea2);
+  }
+  if (X.mine(X_POW2)) {
+    double qx = lane == 1 ? RH : T_surf_K, qy = lane == 1 ? 1.5 : 4.0;             // :1520, :1233
+    if (p.satterlund && lane == 2) { qx = 10.0; qy = 11.4 - 2353.0 / (T_surf + 273.15); }  // :796 (surface)
+    pw2 = pow(qx, qy);
+  }
+  if (X.mine(X_ATAN2) && P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
     at2 = atan(lane == 1 ? T_air + RH : (lane == 2 ? RH - 1.676331 : (lane == 3 ? 0.023101 * RH
                                                                                  : 0.151977 * sqrt(RH + 8.313659))));
-  double e_sat_surf = !p.satterlund ? 0.611 * lane_value(ex2, 0) : lane_value(pw2, 2) / 1000.0;
+  X.put(X_EXP2, ex2);
+  X.put(X_POW2, pw2);
+  X.put(X_ATAN2, at2);
+  if (W > 1) lds_level_barrier();
+  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : X.get(X_POW2, pw2, 2) / 1000.0;
   e_sat_surf = e_sat_surf * 10.0;
-  const double W_p = 1.12 * lane_value(ex2, 1);
+  const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
   const double e_surf = RH * e_sat_surf;
   const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
@@ -512,11 +561,14 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double b_s = -0.0572 - (0.0173 * W_p);
 
   // ---- level 3: after W_p
-  const double ex3 = exp(lane == 1 ? a_s + (b_s * u.m_opt) : a_sa + (b_sa * u.m_opt));  // SF:610, SF:652
-  const double tau = npmin(npmax(lane_value(ex3, 0) - p.dust, 0.0), 1.0);
+  double ex3 = 0.0;
+  if (X.mine(X_EXP3)) ex3 = exp(lane == 1 ? a_s + (b_s * u.m_opt) : a_sa + (b_sa * u.m_opt));  // SF:610, SF:652
+  X.put(X_EXP3, ex3);
+  if (W > 1) lds_level_barrier();
+  const double tau = npmin(npmax(X.get(X_EXP3, ex3, 0) - p.dust, 0.0), 1.0);
   double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos_wl + s.sin_leq * u.sin_d);
   K_ET = npmax(K_ET, 0.0);
-  const double gam_s = (1.0 - lane_value(ex3, 1)) + p.dust;
+  const double gam_s = (1.0 - X.get(X_EXP3, ex3, 1)) + p.dust;
   const double K_dif = 0.5 * gam_s * u.k_et_flat;
   const double K_global = tau * u.k_et_flat + K_dif;
   const double K_bs = 0.5 * gam_s * albedo * K_global;
@@ -529,23 +581,26 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const double term1 = p.one_minus_F_172 * pw_em;
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
-    em_air = 1.08 * (1.0 - lane_value(ex2, 2));
+    em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
   }
   const double LW_in = em_air * p.sigma * pw_ta4;
-  double LW_out = p.em_surf_sigma * lane_value(pw2, 0);
+  double LW_out = p.em_surf_sigma * X.get(X_POW2, pw2, 0);
   LW_out = LW_out + p.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
   // :1314 (Qa = 0; qc = 0 unless the optional conduction term is on)
   const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + qc;
   double T_wb = 0.0;
   if (P_snow > 0.0) {
-    T_wb = T_air * lane_value(at2, 0) + lane_value(at2, 1) - lane_value(at2, 2) +
-           ((0.00391838 * lane_value(pw2, 1)) * lane_value(at2, 3)) - 4.86035;
+    T_wb = T_air * X.get(X_ATAN2, at2, 0) + X.get(X_ATAN2, at2, 1) - X.get(X_ATAN2, at2, 2) +
+           ((0.00391838 * X.get(X_POW2, pw2, 1)) * X.get(X_ATAN2, at2, 3)) - 4.86035;
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
   { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_ET, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
 #endif
+  // No barrier needed before the next step's writes: a slot is rewritten one
+  // step later, after two more level barriers, which every wave reaches only
+  // after reading this step's value of it.
 }
 
 // ---------------------------------------------------------------------------
