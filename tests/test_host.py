@@ -248,6 +248,19 @@ def test_ice_flow_entry_points_reject_bad_arguments_without_a_device():
     assert nat.PREV_DEPTH == -1 and (nat.FLOW_ALL, nat.FLOW_INTERIOR, nat.FLOW_EDGES) == (0, 1, 2)
 
 
+def test_conduction_entry_points_reject_bad_arguments_without_a_device():
+    """The conduction ABI fails cleanly on a null handle (no HIP call is made);
+    the Qc field id follows tfg.h."""
+    from topoflow_glacier import _native as nat
+
+    L = nat.load()
+    assert L.tfg_conduction_update(None, 0.1, 2.1, 30.0, 30.0, 0.0, None, None, 0) == nat.ERR_ARG
+    assert L.tfg_conduction_edges(None, None, None, 0) == nat.ERR_ARG
+    assert L.tfg_conduction_off(None) == nat.ERR_ARG
+    txt = (ROOT / "include" / "tfg.h").read_text()
+    assert "TFG_ST_QC = 24," in txt and nat.FIELD["Qc"] == 24 and "TFG_NUM_FIELDS = 25" in txt
+
+
 def test_library_is_built_from_these_sources():
     """build() keys reuse on content: the in-tree library carries the sha256 of
     exactly the sources and flags it was built from (tfg_build_info), and
