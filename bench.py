@@ -120,6 +120,9 @@ def parse():
     ap.add_argument("--dt", type=float, default=1.0, help="time step [h] (BASELINE config 5: 0.25)")
     ap.add_argument("--catchments", type=int, default=0,
                     help="K > 0: per-catchment mass balance over a K-catchment block raster (BASELINE config 5)")
+    ap.add_argument("--conduction", action="store_true",
+                    help="the optional lateral heat-conduction term: Qc re-evaluated (with the one-row halo swap "
+                         "between ranks) before every fused launch, inside the timed region")
     return ap.parse_args()
 
 
@@ -242,7 +245,7 @@ def pmc_traffic(rows, args):
 
     pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}.json"
     running = nat.code_object_sha256()
-    if args.engine != "float32" or args.catchments or args.dt != 1.0:
+    if args.engine != "float32" or args.catchments or args.dt != 1.0 or args.conduction:
         return None, {"profile": None, "reason": "no PMC profile for this variant of the kernel"}
     if not pmc.exists():
         return None, {"profile": None, "reason": f"{pmc.relative_to(ROOT)} not measured"}
@@ -336,6 +339,17 @@ def main():
         if world > 1:
             dist.barrier()
 
+    cond_ms = []
+
+    def conduct():
+        """The optional conduction term before a launch: edge rows swapped between
+        ranks (RCCL over xGMI), Qc evaluated (k_conduction), 30 m cells."""
+        from topoflow_glacier.sharding import lateral_conduction
+
+        t = time.perf_counter()
+        lateral_conduction(eng, cfg.k_snow, cfg.k_ice, 30.0, 30.0, distributed=world > 1)
+        cond_ms.append((time.perf_counter() - t) * 1e3)
+
     # warmup (untimed)
     eng.run(args.warmup)
     barrier()
@@ -348,6 +362,8 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for i in range(n_launch):
+        if args.conduction:
+            conduct()
         ev[i][0].record(stream)
         eng.run(args.fuse)
         ev[i][1].record(stream)
@@ -415,7 +431,8 @@ def main():
             "config": {
                 "workload": f"{plan['workload']}, {args.dt:g} h steps, "
                             f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch"
-                            + (f", {args.catchments} catchments" if args.catchments else ""),
+                            + (f", {args.catchments} catchments" if args.catchments else "")
+                            + (", lateral conduction re-evaluated before every launch" if args.conduction else ""),
                 "grid_per_gpu": [rows, args.nx],
                 "frames": args.frames,
                 "fuse_steps": args.fuse,
@@ -435,6 +452,7 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_numpy_1core": numpy_leg,
             "pcie_inclusive": pcie,
+            "conduction_host_ms_per_update": (float(np.mean(cond_ms)) if cond_ms else None),
             "sample_parity": parity,
             "mass_balance": {k: float(v) for k, v in zip(["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"], diag[0])},
         }
