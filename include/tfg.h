@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 4
+#define TFG_ABI_VERSION 5
 
 /* status codes */
 enum {
@@ -215,6 +215,20 @@ int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n
  * tfg_set_inputs / tfg_get_outputs. */
 int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
                int dst_dtype, int64_t n);
+
+/* One synchronous step of each of m single-cell TFG_F64 handles, in ONE
+ * launch: for handle hs[i], the same as tfg_update(hs[i], u[i]->frame,
+ * src[i], TFG_F64, u[i], dst[i], TFG_F64, 1), and the same results bit for
+ * bit.  src[i] is that handle's 5 fp64 inputs in tfg_set_inputs order
+ * (P_air, Hum_sp, P, T_air, uz), dst[i] its 8 fp64 outputs in
+ * tfg_get_outputs order.  Every handle must be on one device and share one
+ * stream (tfg_shared_stream), and may appear once.  Errors name the handle's
+ * index and are read with tfg_last_error(NULL); no step runs then.
+ * Replaces: update() (:413-465) of many single-catchment models, one Python
+ * object per catchment as NextGen runs them, when a caller has advanced them
+ * all before reading any (the BMI's `defer_update` mode). */
+int tfg_update_many(tfg_handle* const* hs, int m, const double* const* src, const tfg_uniforms* const* u,
+                    double* const* dst);
 
 /* `index` value for TFG_OUT_H_SNOW / TFG_OUT_H_ICE: the fp64 previous-step
  * depth the next step reads (:895-911 uses the previous depths), rather than a

@@ -2,7 +2,10 @@
 one process, stepped in turn (7 set_value, update, 8 get_value each).  Reports
 creation time and the steady-state per-instance step cost (after one untimed
 round).  Diagnostic only.
-  python tests/diagnostics/bmi_many_instances.py [instances] [steps] [shared] [distinct]"""
+  python tests/diagnostics/bmi_many_instances.py [instances] [steps] [shared] [distinct] [defer] [ensemble]
+  defer     config defer_update: update() queues, the queued models step in one launch
+  ensemble  every model's set_value + update(), then every model's get_value
+            (NextGen's order is per model: set, update, get)"""
 import json
 import sys
 import tempfile
@@ -23,13 +26,17 @@ tmp = Path(tempfile.mkdtemp())
 cfg = tmp / "cfg.yaml"
 cfg.write_text(yaml.dump(BASE_CFG))
 distinct = "distinct" in sys.argv[3:]  # every model its own centroid: no two clocks alike (real catchments)
+defer = "defer" in sys.argv[3:]
+ensemble = "ensemble" in sys.argv[3:]
+base = dict(BASE_CFG, defer_update=defer)
+cfg.write_text(yaml.dump(base))
 t0 = time.perf_counter()
 models = []
 for i in range(n_inst):
     m = BmiTopoflowGlacier()
     if distinct:
         c = tmp / f"cfg{i}.yaml"
-        c.write_text(yaml.dump(dict(BASE_CFG, lat=BASE_CFG["lat"] + 1e-4 * i, lon=BASE_CFG["lon"] - 1e-4 * i)))
+        c.write_text(yaml.dump(dict(base, lat=BASE_CFG["lat"] + 1e-4 * i, lon=BASE_CFG["lon"] - 1e-4 * i)))
         m.initialize(str(c))
     else:
         m.initialize(str(cfg))
@@ -54,9 +61,24 @@ for m in models:
     for k, v in ins.items():
         m.set_value(k, np.array([v]))
     m.update()
+for m in models:
+    m.get_value(outs[0], buf)
 t_set = t_upd = t_get = 0.0
 t0 = time.perf_counter()
-for _ in range(steps):
+for _ in range(steps if ensemble else 0):
+    a = time.perf_counter()
+    for m in models:
+        for k, v in ins.items():
+            m.set_value(k, np.array([v]))
+        m.update()
+    b = time.perf_counter()
+    for m in models:
+        for k in outs:
+            m.get_value(k, buf)
+    c = time.perf_counter()
+    t_upd += b - a  # set_value + update() (queues when deferred)
+    t_get += c - b  # get_value (the first one runs the queued launch when deferred)
+for _ in range(0 if ensemble else steps):
     for m in models:
         a = time.perf_counter()
         for k, v in ins.items():
@@ -89,7 +111,8 @@ ref = models[0].get_value("land_surface_water__runoff_volume_flux", np.zeros(1))
 same = all(m.get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0] == ref for m in models)
 for m in models:
     m.finalize()
-print(json.dumps({"instances": n_inst, "steps": steps, "distinct_clocks": distinct,
+print(json.dumps({"instances": n_inst, "steps": steps, "distinct_clocks": distinct, "defer_update": defer,
+                  "pattern": "ensemble" if ensemble else "interleaved",
                   "extra_shared_stream": "shared" in sys.argv[3:], "create_s": t_create,
                   "us_per_instance_step": t_run / (n_inst * steps) * 1e6,
                   "us_set_update_get": [round(t / (n_inst * steps) * 1e6, 2) for t in (t_set, t_upd, t_get)],

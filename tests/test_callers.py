@@ -190,3 +190,116 @@ def test_many_bmi_instances_in_one_process_interleaved(tmp_path):
         np.testing.assert_array_equal(inter[2 * j], ref, err_msg=p.name)
         np.testing.assert_array_equal(inter[2 * j + 1], ref, err_msg=p.name)
     assert not np.array_equal(inter[0], inter[-1])  # the configs differ
+
+
+@pytest.mark.gpu
+def test_deferred_updates_equal_per_model_updates(tmp_path, monkeypatch):
+    """``defer_update``: fourteen single-catchment models (the six catchment
+    configs and one with SATTERLUND and the ground heat flux, twice each)
+    stepped as an ensemble -- every model's inputs and
+    update(), then every model's outputs -- advance in ONE tfg_update_many
+    launch per step (k_cell_many).  Outputs every step, the cold contents,
+    albedo, the mass-balance integrals and the clock equal those of models
+    stepped one tfg_update at a time, bit for bit.  So do the interleaved
+    pattern (each model read right after its update: batches of one), a
+    model on its own stream (its own batch), update_until after a queued
+    step, and finalize with a step queued."""
+    from pathlib import Path
+
+    from topoflow_glacier import BmiTopoflowGlacier, _native
+    from topoflow_glacier.bmi import bmi_topoflow_glacier as B
+    from topoflow_glacier.engine import UpdateBatch, update_many
+    from topoflow_glacier.forcing import read_forcing_csv
+    from tests.harness import ROOT
+
+    cfgs = sorted((ROOT / "tests" / "golden" / "config").glob("cat-*.yaml"))
+    extra = tmp_path / "satterlund_qg.yaml"  # the alternative vapour formulas and a nonzero Qc
+    extra.write_text(yaml.dump(dict(BASE_CFG, SATTERLUND=True, ground_heat_flux=True)))
+    cfgs.append(extra)
+    deferred = []
+    for p in cfgs:
+        c = yaml.safe_load(p.read_text())
+        c["defer_update"] = True
+        q = tmp_path / ("deferred_" + p.name)
+        q.write_text(yaml.dump(c))
+        deferred.append(q)
+    t = read_forcing_csv(CSV, BASE_CFG["start_time"], BASE_CFG["end_time"])
+    nsteps = 30
+    names = ["snowpack__depth", "snowpack__liquid-equivalent_depth", "snowpack__melt_volume_flux",
+             "glacier_ice__thickness", "glacier__liquid_equivalent_depth", "glacier_ice__melt_volume_flux",
+             "land_surface_water__runoff_volume_flux", "atmosphere_bottom_air_water-vapor__relative_saturation"]
+    batches: list[int] = []
+    run = UpdateBatch.run
+
+    def counting(self):
+        batches.append(len(self))
+        run(self)
+
+    monkeypatch.setattr(UpdateBatch, "run", counting)
+
+    def make(p: Path):
+        m = BmiTopoflowGlacier()
+        m.initialize(p)
+        return m
+
+    def final(m):
+        return [m.get_current_time(), float(m.Eccs[0]), float(m.Ecci[0]), float(m.albedo[0]), float(m.n[0]),
+                float(m.vol_SM[0]), float(m.vol_IM[0]), float(m.vol_P[0]), float(m.P_max[0])]
+
+    def interleaved(models):
+        rec = [[] for _ in models]
+        for i in range(nsteps):
+            for j, m in enumerate(models):
+                t.apply(m, i)
+                m.update()
+                rec[j].append([m.get_value(v, np.zeros(1))[0] for v in names])
+        return [np.array(r) for r in rec], [final(m) for m in models]
+
+    def ensemble(models):
+        rec = [[] for _ in models]
+        for i in range(nsteps):
+            for m in models:
+                t.apply(m, i)
+                m.update()
+            for j, m in enumerate(models):
+                rec[j].append([m.get_value(v, np.zeros(1))[0] for v in names])
+        return [np.array(r) for r in rec], [final(m) for m in models]
+
+    ref_models = [make(p) for p in cfgs for _ in range(2)]
+    ref, ref_final = interleaved(ref_models)
+    assert batches == []  # not deferred: one tfg_update per step
+    for m in ref_models:
+        m.finalize()
+
+    models = [make(p) for p in deferred for _ in range(2)]
+    models[-1]._engine.set_stream(None)  # its own stream: a batch of its own
+    got, got_final = ensemble(models)
+    assert batches[:2] == [2 * len(cfgs) - 1, 1] and len(batches) == 2 * nsteps
+    for j in range(len(models)):
+        np.testing.assert_array_equal(got[j], ref[j], err_msg=str(j))
+    assert got_final == ref_final
+    # interleaved on deferred models: batches of one, the same results
+    batches.clear()
+    models2 = [make(p) for p in deferred for _ in range(2)]
+    got2, got2_final = interleaved(models2)
+    assert set(batches) == {1}
+    for j in range(len(models2)):
+        np.testing.assert_array_equal(got2[j], ref[j], err_msg=str(j))
+    assert got2_final == ref_final
+    # update_until after a queued step, then finalize with a step queued
+    t.apply(models[0], nsteps)
+    models[0].update()
+    models[0].update_until(models[0].get_current_time() + 2 * models[0].get_time_step())
+    assert models[0].get_current_time() == (nsteps + 3) * models[0].get_time_step()
+    t.apply(models[1], nsteps)
+    models[1].update()
+    for m in models + models2:
+        m.finalize()
+    assert not B._BATCHES
+    # a handle may appear once per call
+    e = make(deferred[0])
+    k = e._engine.step_index
+    with pytest.raises(_native.NativeError, match="listed twice"):
+        update_many([e._engine, e._engine], [e._in_block] * 2, [e._out_block] * 2)
+    assert e._engine.step_index == k  # no step ran
+    e.finalize()

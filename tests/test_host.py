@@ -142,7 +142,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 17
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.tfg_abi_version() == 4
+    assert L.tfg_abi_version() == _native.ABI_VERSION == 5
     assert b"gfx950" in L.tfg_build_info()
 
 
@@ -259,6 +259,23 @@ def test_conduction_entry_points_reject_bad_arguments_without_a_device():
     assert L.tfg_conduction_off(None) == nat.ERR_ARG
     txt = (ROOT / "include" / "tfg.h").read_text()
     assert "TFG_ST_QC = 24," in txt and nat.FIELD["Qc"] == 24 and "TFG_NUM_FIELDS = 25" in txt
+
+
+def test_update_many_rejects_bad_arguments_without_a_device():
+    """tfg_update_many: an empty batch is a no-op; null arrays or a null
+    handle fail with TFG_ERR_ARG and a message naming the handle's index,
+    before any HIP call."""
+    import ctypes
+
+    from topoflow_glacier import _native as nat
+
+    L = nat.load()
+    assert L.tfg_update_many(None, 0, None, None, None) == nat.OK
+    assert L.tfg_update_many(None, 2, None, None, None) == nat.ERR_ARG
+    hs = (ctypes.c_void_p * 2)(None, None)
+    p = (ctypes.c_void_p * 2)(None, None)
+    assert L.tfg_update_many(hs, 2, p, p, p) == nat.ERR_ARG
+    assert b"handle 0" in L.tfg_last_error(None)
 
 
 def test_library_is_built_from_these_sources():

@@ -515,20 +515,11 @@ struct CellIo {
   double in[kNumForc];  // P, T_air, Hum_sp, P_air, uz (device frame order)
 };
 
-__global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, const CellIo io, const double* __restrict__ geo,
-                                             const int32_t* __restrict__ catch_id, double* __restrict__ st,
-                                             int64_t* __restrict__ tot, int32_t* __restrict__ ring,
-                                             double* __restrict__ forc, double* __restrict__ hist,
-                                             double* __restrict__ slab, const double* __restrict__ qcf,
-                                             int read_depths) {
-  __shared__ double lds_x[tfg::X_SLOTS * 4];
-  const DevParams& p = a.p;
-  const int64_t np = a.n_pad;
-  const tfg_uniforms& u = io.u;
-#ifdef TFG_CELL_TIMING  // diagnostic build: phase times [wall-clock ticks] replace the outputs
-  const long long tt0 = wall_clock64();
-#endif
-  CellState cs;
+// The one cell's fp64 state (the depths read or re-derived as k_fused does)
+// and its static geometry (k_prepare_static's planes).
+__device__ __forceinline__ void load_one_cell(const DevParams& p, int64_t np, const double* __restrict__ st,
+                                              const int64_t* __restrict__ tot, const double* __restrict__ geo,
+                                              int read_depths, CellState& cs, CellStatic& sx) {
   cs.h_swe = st[S_HSWE * np];
   cs.h_iwe = st[S_HIWE * np];
   cs.Eccs = st[S_ECCS * np];
@@ -543,8 +534,47 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, co
     cs.h_ice = cs.h_iwe * p.wi;   // :1726
   }
   cs.tot_q = tot[0];
+  sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
+}
+
+// Write the state back and add the step(s)' diagnostics to the slab row `srow`
+// (whose values at kernel start were `sv`) as k_fused accumulates them: the
+// wave and workgroup sums of one cell add zeros.
+__device__ __forceinline__ void store_one_cell(int64_t np, const CellState& cs, const CellDiag& d, const double (&sv)[6],
+                                               double* __restrict__ st, int64_t* __restrict__ tot,
+                                               double* __restrict__ srow) {
+  st[S_HSWE * np] = cs.h_swe;
+  st[S_HIWE * np] = cs.h_iwe;
+  st[S_ECCS * np] = cs.Eccs;
+  st[S_ECCI * np] = cs.Ecci;
+  st[S_N * np] = cs.n;
+  st[S_ALB * np] = cs.albedo;
+  tot[0] = cs.tot_q;
+  srow[0] = sv[0] + d.P;
+  srow[1] = sv[1] + d.PR;
+  srow[2] = sv[2] + d.PS;
+  srow[3] = sv[3] + d.SM;
+  srow[4] = sv[4] + d.IM;
+  srow[5] = tfg::npmax(sv[5], d.Pmax);
+}
+
+__global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, const CellIo io, const double* __restrict__ geo,
+                                             const int32_t* __restrict__ catch_id, double* __restrict__ st,
+                                             int64_t* __restrict__ tot, int32_t* __restrict__ ring,
+                                             double* __restrict__ forc, double* __restrict__ hist,
+                                             double* __restrict__ slab, const double* __restrict__ qcf,
+                                             int read_depths) {
+  __shared__ double lds_x[tfg::X_SLOTS * 4];
+  const DevParams& p = a.p;
+  const int64_t np = a.n_pad;
+  const tfg_uniforms& u = io.u;
+#ifdef TFG_CELL_TIMING  // diagnostic build: phase times [wall-clock ticks] replace the outputs
+  const long long tt0 = wall_clock64();
+#endif
+  CellState cs;
+  CellStatic sx;
+  load_one_cell(p, np, st, tot, geo, read_depths, cs, sx);
   const int32_t q_old = ring[(int64_t)u.slot * np];
-  const CellStatic sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
   double* srow = slab + (catch_id ? catch_id[0] : 0) * 6;
   double sv[6];
 #pragma unroll
@@ -577,13 +607,7 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, co
     double* fr = forc + (int64_t)u.frame * kNumForc * np;
 #pragma unroll
     for (int f = 0; f < kNumForc; ++f) fr[f * np] = io.in[f];
-    st[S_HSWE * np] = cs.h_swe;
-    st[S_HIWE * np] = cs.h_iwe;
-    st[S_ECCS * np] = cs.Eccs;
-    st[S_ECCI * np] = cs.Ecci;
-    st[S_N * np] = cs.n;
-    st[S_ALB * np] = cs.albedo;
-    tot[0] = cs.tot_q;
+    store_one_cell(np, cs, d, sv, st, tot, srow);
     double* out = a.io_out;  // [8][1]: h_snow, h_swe, SM, h_ice, h_iwe, IM, M_total, RH
     out[0] = o.h_snow;
     out[1] = cs.h_swe;
@@ -593,14 +617,6 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell(const KArgs a, co
     out[5] = o.IM;
     out[6] = o.M_total;
     out[7] = o.RH;
-    // the slab row as k_fused accumulates it (wave and workgroup sums of one
-    // cell add zeros)
-    srow[0] = sv[0] + d.P;
-    srow[1] = sv[1] + d.PR;
-    srow[2] = sv[2] + d.PS;
-    srow[3] = sv[3] + d.SM;
-    srow[4] = sv[4] + d.IM;
-    srow[5] = tfg::npmax(sv[5], d.Pmax);
 #ifdef TFG_CELL_TIMING
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const long long tt3 = wall_clock64();
@@ -631,21 +647,8 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell_run(const KArgs a
   const DevParams& p = a.p;
   const int64_t np = a.n_pad;
   CellState cs;
-  cs.h_swe = st[S_HSWE * np];
-  cs.h_iwe = st[S_HIWE * np];
-  cs.Eccs = st[S_ECCS * np];
-  cs.Ecci = st[S_ECCI * np];
-  cs.n = st[S_N * np];
-  cs.albedo = st[S_ALB * np];
-  if (read_depths) {
-    cs.h_snow = st[S_HSNOW * np];
-    cs.h_ice = st[S_HICE * np];
-  } else {
-    cs.h_snow = cs.h_swe * p.ws;  // :1711, bit-identical to the last step
-    cs.h_ice = cs.h_iwe * p.wi;   // :1726
-  }
-  cs.tot_q = tot[0];
-  const CellStatic sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
+  CellStatic sx;
+  load_one_cell(p, np, st, tot, geo, read_depths, cs, sx);
   double* srow = slab + (catch_id ? catch_id[0] : 0) * 6;
   double sv[6];
 #pragma unroll
@@ -683,19 +686,91 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell_run(const KArgs a
     h[H_RH * np] = o.RH;
     cur = nxt;
   }
-  st[S_HSWE * np] = cs.h_swe;
-  st[S_HIWE * np] = cs.h_iwe;
-  st[S_ECCS * np] = cs.Eccs;
-  st[S_ECCI * np] = cs.Ecci;
-  st[S_N * np] = cs.n;
-  st[S_ALB * np] = cs.albedo;
-  tot[0] = cs.tot_q;
-  srow[0] = sv[0] + d.P;  // the slab row as k_fused accumulates it
-  srow[1] = sv[1] + d.PR;
-  srow[2] = sv[2] + d.PS;
-  srow[3] = sv[3] + d.SM;
-  srow[4] = sv[4] + d.IM;
-  srow[5] = tfg::npmax(sv[5], d.Pmax);
+  store_one_cell(np, cs, d, sv, st, tot, srow);
+}
+
+// One step of many one-cell fp64 handles in one launch (tfg_update_many: the
+// per-catchment BMI models of a process that have each been asked for a step;
+// NextGen-style ensembles stepped together).  Workgroup j runs job j exactly
+// as k_cell runs its one handle: the job record (the handle's DevParams and
+// buffers, the step's uniforms and inputs) sits in a pinned, device-mapped
+// host block; the workgroup stages it into LDS with one coalesced read, so
+// every later uniform read is an LDS broadcast instead of a PCIe round trip.
+struct CellJob {
+  DevParams p;
+  tfg_uniforms u;
+  double in[kNumForc];  // P, T_air, Hum_sp, P_air, uz (device frame order)
+  const double* geo;
+  const int32_t* catch_id;
+  double* st;
+  int64_t* tot;
+  int32_t* ring;
+  double* forc;
+  double* hist;
+  double* slab;
+  const double* qc;  // null while the conduction term is off
+  int64_t n_pad;
+  int32_t read_depths;
+  int32_t pad_;
+};
+static_assert(sizeof(CellJob) % 8 == 0, "CellJob is staged as 8-byte words");
+
+__global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell_many(const CellJob* __restrict__ jobs,
+                                                  double* __restrict__ out, uint32_t* __restrict__ flags,
+                                                  uint32_t seq) {
+  __shared__ double lds_x[tfg::X_SLOTS * 4];
+  __shared__ CellJob job;
+  {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(jobs + blockIdx.x);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(&job);
+    for (int i = threadIdx.x; i < (int)(sizeof(CellJob) / 8); i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const DevParams& p = job.p;
+  const int64_t np = job.n_pad;
+  double* const st = job.st;
+  int64_t* const tot = job.tot;
+  int32_t* const ring = job.ring;
+  CellState cs;
+  CellStatic sx;
+  load_one_cell(p, np, st, tot, job.geo, job.read_depths, cs, sx);
+  const int32_t q_old = ring[(int64_t)job.u.slot * np];
+  double* srow = job.slab + (job.catch_id ? job.catch_id[0] : 0) * 6;
+  double sv[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) sv[i] = srow[i];
+  const double qc = job.qc ? job.qc[0] : 0.0;
+  CellDiag d;
+  diag_zero(d);
+  CellOut o;
+  int32_t q_new;
+  tfg::cell_step_exact_wave<tfg::kCellWaves>(p, sx, job.u, job.in[F_P], job.in[F_T], job.in[F_Q], job.in[F_PA],
+                                              job.in[F_UZ], q_old, q_new, cs, o, d, qc, lds_x);
+  if (threadIdx.x == 0) {
+    ring[(int64_t)job.u.slot * np] = q_new;
+    double* h = job.hist + (int64_t)job.u.hist * kNumHist * np;
+    h[H_HSNOW * np] = o.h_snow;
+    h[H_SM * np] = o.SM;
+    h[H_HICE * np] = o.h_ice;
+    h[H_IM * np] = o.IM;
+    h[H_MTOT * np] = o.M_total;
+    h[H_RH * np] = o.RH;
+    double* fr = job.forc + (int64_t)job.u.frame * kNumForc * np;
+#pragma unroll
+    for (int f = 0; f < kNumForc; ++f) fr[f * np] = job.in[f];
+    store_one_cell(np, cs, d, sv, st, tot, srow);
+    double* ob = out + (int64_t)blockIdx.x * 8;  // h_snow, h_swe, SM, h_ice, h_iwe, IM, M_total, RH
+    ob[0] = o.h_snow;
+    ob[1] = cs.h_swe;
+    ob[2] = o.SM;
+    ob[3] = o.h_ice;
+    ob[4] = cs.h_iwe;
+    ob[5] = o.IM;
+    ob[6] = o.M_total;
+    ob[7] = o.RH;
+    __threadfence_system();
+    __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Per-cell solar geometry of the fast engine, once per static-raster change:
@@ -1975,6 +2050,106 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
 #ifdef TFG_UPDATE_TIMING
   g_upd_ns[4] += 1;
 #endif
+  return TFG_OK;
+}
+
+namespace {
+// tfg_update_many's pinned, device-mapped block of one device:
+// [jobs m x CellJob | outputs m x 8 f64 | release flags m x u32].  Calls are
+// synchronous, so one block per device serves every call, under its mutex.
+struct ManyBlock {
+  std::mutex mu;
+  char* h = nullptr;
+  char* d = nullptr;
+  size_t cap = 0;
+  uint32_t seq = 0;
+};
+constexpr int kMaxDevices = 64;
+ManyBlock g_many[kMaxDevices];
+}  // namespace
+
+int tfg_update_many(tfg_handle* const* hs, int m, const double* const* src, const tfg_uniforms* const* u,
+                    double* const* dst) {
+  if (m <= 0) return TFG_OK;
+  if (!hs || !src || !u || !dst) return fail(nullptr, TFG_ERR_ARG, "tfg_update_many: null argument");
+  tfg_handle* h0 = hs[0];
+  if (!h0) return fail(nullptr, TFG_ERR_ARG, "tfg_update_many: null handle 0");
+  if (h0->device < 0 || h0->device >= kMaxDevices) return fail(nullptr, TFG_ERR_ARG, "tfg_update_many: device id");
+  for (int i = 0; i < m; ++i) {
+    tfg_handle* h = hs[i];
+    const std::string at = "tfg_update_many: handle " + std::to_string(i) + ": ";
+    if (!h || !src[i] || !u[i] || !dst[i]) return fail(nullptr, TFG_ERR_ARG, at + "null handle/src/uniforms/dst");
+    if (h->engine != TFG_F64 || h->n != 1) return fail(nullptr, TFG_ERR_ARG, at + "not a one-cell TFG_F64 handle");
+    if (h->device != h0->device || h->stream != h0->stream)
+      return fail(nullptr, TFG_ERR_ARG, at + "every handle must be on one device and share one stream (tfg_shared_stream)");
+    if (int rc = check_step(h, u[i], 1)) return fail(nullptr, rc, at + h->err);
+  }
+  {  // one step per handle per launch: a handle listed twice would race with itself
+    std::vector<const tfg_handle*> v(hs, hs + m);
+    std::sort(v.begin(), v.end());
+    if (std::adjacent_find(v.begin(), v.end()) != v.end())
+      return fail(nullptr, TFG_ERR_ARG, "tfg_update_many: a handle is listed twice");
+  }
+  ManyBlock& B = g_many[h0->device];
+  std::lock_guard<std::mutex> lock(B.mu);
+  HIPCHK(nullptr, hipSetDevice(h0->device));
+  const size_t job_b = (size_t)m * sizeof(CellJob);
+  const size_t out_off = (job_b + 255) & ~(size_t)255;
+  const size_t flag_off = (out_off + (size_t)m * 64 + 255) & ~(size_t)255;
+  const size_t total = flag_off + (size_t)m * 4;
+  if (B.cap < total) {
+    const size_t want = std::max(total, B.cap * 2);
+    if (B.h) HIPCHK(nullptr, hipHostFree(B.h));
+    B.h = B.d = nullptr;
+    B.cap = 0;
+    HIPCHK(nullptr, hipHostMalloc((void**)&B.h, want, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(B.h, 0, want);
+    HIPCHK(nullptr, hipHostGetDevicePointer((void**)&B.d, B.h, 0));
+    B.cap = want;
+    B.seq = 0;
+  }
+  CellJob* jobs = reinterpret_cast<CellJob*>(B.h);
+  static const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};  // BMI order -> device frame order
+  for (int i = 0; i < m; ++i) {
+    tfg_handle* h = hs[i];
+    if (int rc = prepare_steps(h)) return fail(nullptr, rc, "tfg_update_many: " + h->err);
+    CellJob& j = jobs[i];
+    j.p = h->dp;
+    j.u = *u[i];
+    for (int f = 0; f < 5; ++f) j.in[map[f]] = src[i][f];
+    j.geo = reinterpret_cast<const double*>(h->geo);
+    j.catch_id = h->catch_id;
+    j.st = h->st;
+    j.tot = h->tot;
+    j.ring = h->ring;
+    j.forc = static_cast<double*>(h->forc);
+    j.hist = static_cast<double*>(h->hist);
+    j.slab = h->slab;
+    j.qc = h->qc_on ? static_cast<const double*>(h->qc) : nullptr;
+    j.n_pad = h->n_pad;
+    j.read_depths = h->depths_derived ? 0 : 1;
+    j.pad_ = 0;
+  }
+  const uint32_t seq = ++B.seq == 0 ? ++B.seq : B.seq;  // never 0, the initial flag value
+  hipLaunchKernelGGL(k_cell_many, m, 64 * tfg::kCellWaves, 0, h0->stream, reinterpret_cast<const CellJob*>(B.d),
+                     reinterpret_cast<double*>(B.d + out_off), reinterpret_cast<uint32_t*>(B.d + flag_off), seq);
+  HIPCHK(nullptr, hipGetLastError());
+  for (int i = 0; i < m; ++i) {
+    hs[i]->depths_derived = true;
+    hs[i]->last_hist = u[i]->hist;
+  }
+  // wait for every workgroup's release flag (a stream synchronisation after ~2 ms)
+  const volatile uint32_t* fl = reinterpret_cast<const volatile uint32_t*>(B.h + flag_off);
+  const auto t0 = std::chrono::steady_clock::now();
+  int done = 0;
+  for (int64_t spins = 0; done < m; ++spins) {
+    while (done < m && fl[done] == seq) ++done;
+    if (done < m && (spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+  }
+  if (done == m) std::atomic_thread_fence(std::memory_order_acquire);
+  else HIPCHK(nullptr, hipStreamSynchronize(h0->stream));
+  const double* oh = reinterpret_cast<const double*>(B.h + out_off);
+  for (int i = 0; i < m; ++i) std::memcpy(dst[i], oh + (size_t)i * 8, 64);
   return TFG_OK;
 }
 

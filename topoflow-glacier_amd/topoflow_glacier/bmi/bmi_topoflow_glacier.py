@@ -10,6 +10,11 @@ Modes
   * single catchment (the reference's case, ny = nx = 1): fp64 engine with the
     reference's operation order; inputs/outputs mirrored eagerly, so
     ``get_value_ptr`` references stay live exactly as in the reference.
+    With ``defer_update: true`` update() queues the step instead, and every
+    queued model of the process advances in one launch (tfg_update_many) at
+    the first BMI call that reads or writes one of them, or at
+    :func:`flush_updates`; a held ``get_value_ptr`` array shows the new values
+    from then on.
   * grid (``ny``/``nx`` in the YAML): fp32 engine by default; BMI arrays have
     ny*nx float64 entries, refreshed from the device when read.
 
@@ -28,14 +33,14 @@ import numpy as np
 import yaml
 
 from .. import _native as nat
-from ..engine import GlacierEngine
+from ..engine import GlacierEngine, UpdateBatch
 from ..physics.clock import parse_time
 from ..physics.context import Context, build_context
 from .bmi_base import BmiBase
 from .config import TopoflowGlacierConfig
 from .logger import configure_logging, logger
 
-__all__ = ["BmiTopoflowGlacier"]
+__all__ = ["BmiTopoflowGlacier", "flush_updates"]
 
 # bmi_topoflow_glacier.py:18-37 (names, units, order)
 _dynamic_input_vars = [
@@ -147,6 +152,35 @@ def _shared_stream(device: int) -> int:
     return _SHARED_STREAMS[device]
 
 
+# Queued update() steps of single-catchment models (config ``defer_update``),
+# one batch per device and stream.
+_BATCHES: dict = {}
+
+
+def flush_updates() -> None:
+    """Run every queued ``update()`` of the process (``defer_update`` models):
+    one tfg_update_many launch per device and stream advances them all, with
+    the results of as many tfg_update calls bit for bit.  Called by the first
+    BMI call that reads or writes a queued model; callers may also call it."""
+    if not _BATCHES:
+        return
+    batches = list(_BATCHES.values())
+    _BATCHES.clear()
+    err = None
+    for b in batches:
+        owners = b.owners
+        for m in owners:
+            m._queued = False
+        try:
+            b.run()
+        except Exception as e:  # no step of this batch ran: its models stay at the previous step
+            for m in owners:
+                m._timestep -= 1
+            err = err or e
+    if err is not None:
+        raise err
+
+
 def make_engine(cfg, n_frames: int = 1, hist_depth: int = 1) -> GlacierEngine:
     """The device shard a config describes (fp64 engine for one cell, fp32 for grids)."""
     engine = cfg.engine or ("float64" if cfg.ny * cfg.nx == 1 else "float32")
@@ -189,6 +223,8 @@ class BmiTopoflowGlacier(BmiBase):
         self._engine: GlacierEngine | None = None
         self._stale: set[str] = set()
         self._beta_invalid = False
+        self._defer = False
+        self._queued = False
         configure_logging()
 
     # reference properties (:124-272)
@@ -276,6 +312,9 @@ class BmiTopoflowGlacier(BmiBase):
         self.start_time = start
         self._cal = (0, start, start.year, None, None, None)
         self._clock = self._engine.clock
+        self._defer = bool(cfg.defer_update) and n == 1 and self._engine.engine == "float64"
+        self._in_addr, self._out_addr = self._in_block.ctypes.data, self._out_block.ctypes.data
+        self._queued = False
 
     # ----------------------------------------------------------------- update
     def _require(self) -> GlacierEngine:
@@ -359,11 +398,23 @@ class BmiTopoflowGlacier(BmiBase):
             eng.run(1)
             self._after_steps(1)
             return
+        if self._queued:  # defer_update: this model's previous step first
+            flush_updates()
         if self._dirty_outputs:
             self._push_dirty_outputs()
         self._flow_if_due()
         self._conduct_if_due()
-        eng.update_io(self._in_block, self._out_block)  # the outputs land in the BMI variables
+        if self._defer:
+            # queued: runs with every other queued model of the process in one
+            # launch when one of them is next read or written (flush_updates)
+            key = eng._stream_key()
+            b = _BATCHES.get(key)
+            if b is None:
+                b = _BATCHES[key] = UpdateBatch()
+            b.add_addresses(eng, self._in_addr, self._out_addr, self)
+            self._queued = True
+        else:
+            eng.update_io(self._in_block, self._out_block)  # the outputs land in the BMI variables
         self._timestep += 1
         self._stale.clear()
 
@@ -379,6 +430,8 @@ class BmiTopoflowGlacier(BmiBase):
         if n_steps <= 0:
             return None
         eng = self._require()
+        if self._queued:
+            flush_updates()
         self._push_inputs()
         done = 0
         while done < n_steps:  # in chunks that end where a split term (ice flow, conduction) is due
@@ -391,6 +444,8 @@ class BmiTopoflowGlacier(BmiBase):
 
     def finalize(self) -> None:
         """Release the device shard (reference :467-469)."""
+        if self._queued:
+            flush_updates()
         if self._engine is not None:
             for name in list(self._stale):
                 self._refresh(name)
@@ -409,6 +464,8 @@ class BmiTopoflowGlacier(BmiBase):
         self._stale.discard(internal)
 
     def _mirror(self, external: str) -> np.ndarray:
+        if self._queued:
+            flush_updates()
         hit = getattr(self, "_arrays", {}).get(external)
         if hit is not None:
             internal = hit[1]
@@ -453,6 +510,8 @@ class BmiTopoflowGlacier(BmiBase):
             self._beta_invalid = True
 
     def set_value(self, name: str, src) -> None:
+        if self._queued:  # the queued step reads this model's input block
+            flush_updates()
         if name in _STATIC_FIELD:
             self._static.set_value(name, src)
             self._set_static(name)
@@ -470,6 +529,8 @@ class BmiTopoflowGlacier(BmiBase):
             self._dirty_outputs.add(internal)
 
     def set_value_at_indices(self, name: str, inds, src) -> None:
+        if self._queued:
+            flush_updates()
         if name in _STATIC_FIELD:
             self._static.set_value_at_indices(name, np.asarray(inds), np.asarray(src))
             self._set_static(name)
@@ -556,7 +617,13 @@ class BmiTopoflowGlacier(BmiBase):
         return (parse_time(self.cfg.end_time) - parse_time(self.cfg.start_time)).total_seconds()
 
     # ------------------------------------------------- diagnostics / state
+    def _settled(self) -> GlacierEngine:
+        if self._queued:
+            flush_updates()
+        return self._engine
+
     def _diag(self, i: int) -> np.ndarray:
+        self._settled()
         return np.array([self._engine.diagnostics()[:, i].sum() if i < 5 else self._engine.diagnostics()[:, i].max()])
 
     vol_P = property(lambda self: self._diag(0), doc="sum(P*da*dt) (:558-568)")
@@ -565,7 +632,7 @@ class BmiTopoflowGlacier(BmiBase):
     vol_SM = property(lambda self: self._diag(3), doc="sum(SM*da*dt*3600) (:1482-1487)")
     vol_IM = property(lambda self: self._diag(4), doc="sum(IM*da*dt*3600) (:1489-1494)")
     P_max = property(lambda self: self._diag(5), doc="max P (:570-576)")
-    Eccs = property(lambda self: self._engine.get_field("Eccs"), doc="snowpack cold content [J m-2]")
-    Ecci = property(lambda self: self._engine.get_field("Ecci"), doc="ice cold content [J m-2]")
-    albedo = property(lambda self: self._engine.get_field("albedo"), doc="surface albedo")
-    n = property(lambda self: self._engine.get_field("n"), doc="days since last major snowfall")
+    Eccs = property(lambda self: self._settled().get_field("Eccs"), doc="snowpack cold content [J m-2]")
+    Ecci = property(lambda self: self._settled().get_field("Ecci"), doc="ice cold content [J m-2]")
+    albedo = property(lambda self: self._settled().get_field("albedo"), doc="surface albedo")
+    n = property(lambda self: self._settled().get_field("n"), doc="days since last major snowfall")

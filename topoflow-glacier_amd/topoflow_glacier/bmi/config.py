@@ -22,7 +22,10 @@ deliberate, additive differences:
   ``lateral_conduction`` / ``conduction_interval`` / ``k_snow`` / ``k_ice``
   (the optional lateral heat-conduction term, re-evaluated every
   ``conduction_interval`` steps) and ``ground_heat_flux`` (adds the declared
-  ``geothermal_heat_flux`` to every cell's conduction flux).
+  ``geothermal_heat_flux`` to every cell's conduction flux), and
+  ``defer_update`` (single catchment: ``update()`` queues the step, and the
+  steps of every waiting model of the process run in one launch at the first
+  call that reads or writes one of them; off by default).
 
 Unknown keys are ignored, as in the reference (pydantic default).
 """
@@ -132,6 +135,11 @@ class TopoflowGlacierConfig(BaseModel):
     # optional ground heat flux: the declared but unused geothermal flux Qg
     # (geothermal_heat_flux [J yr-1 m-2], reference :333) added to every cell's Qc
     ground_heat_flux: bool = False
+    # single-catchment models: update() queues the step; all queued models of
+    # the process advance together in one launch (tfg_update_many) when one of
+    # them is next read or written.  Off by default: update() then returns with
+    # the outputs in place, as the reference's does.
+    defer_update: bool = False
 
     @model_validator(mode="after")
     def _flow_needs_spacing(self):

@@ -19,7 +19,7 @@ import numpy as np
 from . import _native as nat
 from .physics.clock import StepClock
 
-__all__ = ["GlacierEngine", "params_from_config"]
+__all__ = ["GlacierEngine", "UpdateBatch", "params_from_config", "update_many"]
 
 _ENGINES = {"float32": nat.F32, "float64": nat.F64}
 _NP = {nat.F32: np.float32, nat.F64: np.float64}
@@ -248,6 +248,13 @@ class GlacierEngine:
         if values.shape != (5, self.n) or out.shape != (8, self.n) or values.dtype != np.float64 \
                 or out.dtype != np.float64 or not (values.flags.c_contiguous and out.flags.c_contiguous):
             raise ValueError(f"update_io needs C-contiguous float64 [5][{self.n}] and [8][{self.n}]")
+        frame, uptr, keep = self._next_uniform()
+        self._chk(self.lib.tfg_update(self.h, frame, values.ctypes.data, nat.F64, uptr, out.ctypes.data, nat.F64, self.n))
+        self.step_index += 1
+        return out
+
+    def _next_uniform(self):
+        """(frame, address of the next step's uniform record, owner of that record)."""
         k0 = self.step_index
         frame = k0 % self.n_frames
         if self.n_frames == 1 and self.hist_depth == 1:
@@ -257,20 +264,22 @@ class GlacierEngine:
             if cache is None or cache[0] != b0:
                 cache = (b0, self.clock.uniform_block(b0, self._UBLOCK))
                 self._ucache = cache
-            uptr = cache[1].ctypes.data + (k0 - b0) * nat.UNIFORM_DTYPE.itemsize
-            keep = None
-        else:
-            keep = np.ascontiguousarray(self.uniforms(1), dtype=nat.UNIFORM_DTYPE)
-            uptr = keep.ctypes.data
-        self._chk(self.lib.tfg_update(self.h, frame, values.ctypes.data, nat.F64, uptr, out.ctypes.data, nat.F64, self.n))
-        self.step_index += 1
-        return out
+            return frame, cache[1].ctypes.data + (k0 - b0) * nat.UNIFORM_DTYPE.itemsize, cache[1]
+        keep = np.ascontiguousarray(self.uniforms(1), dtype=nat.UNIFORM_DTYPE)
+        return frame, keep.ctypes.data, keep
+
+    def _stream_key(self):
+        """Engines with equal keys may step in one tfg_update_many call (one
+        device, one stream; a handle's own stream is its alone)."""
+        s = getattr(self, "_stream_ptr", None)
+        return self.device, s if s else ("own", self.h.value)
 
     def sync(self) -> None:
         self._chk(self.lib.tfg_sync(self.h))
 
     def set_stream(self, stream_ptr: int | None) -> None:
         self._chk(self.lib.tfg_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)))
+        self._stream_ptr = stream_ptr or None
 
     def stream(self) -> int:
         s = ctypes.c_void_p()
@@ -428,3 +437,75 @@ class GlacierEngine:
 
     def reset_diagnostics(self) -> None:
         self._chk(self.lib.tfg_reset_diag(self.h))
+
+
+
+class UpdateBatch:
+    """Single steps of one-cell fp64 engines that share a device and a stream,
+    queued by :meth:`add` and run together by :meth:`run`: one
+    tfg_update_many call, one launch (k_cell_many), the results of as many
+    ``update_io`` calls bit for bit.  An engine may be queued once per run."""
+
+    __slots__ = ("engines", "h", "src", "u", "dst", "keep", "owners")
+
+    def __init__(self):
+        self.engines, self.h, self.src, self.u, self.dst, self.keep, self.owners = [], [], [], [], [], [], []
+
+    def __len__(self) -> int:
+        return len(self.h)
+
+    def add(self, e: GlacierEngine, values: np.ndarray, out: np.ndarray, owner=None) -> None:
+        """Queue the next step of `e`: inputs values [5][1] (P_air, Hum_sp, P,
+        T_air, uz), outputs out [8][1] (h_snow, h_swe, SM, h_ice, h_iwe, IM,
+        M_total, RH), C-contiguous float64 host arrays that must stay alive and
+        unmodified until run() returns (it reads and fills them)."""
+        if e.n != 1 or e.dtype_code != nat.F64:
+            raise ValueError("UpdateBatch: one-cell float64 engines only")
+        if values.dtype != np.float64 or out.dtype != np.float64 or values.size != 5 or out.size != 8 \
+                or not (values.flags.c_contiguous and out.flags.c_contiguous):
+            raise ValueError("UpdateBatch: C-contiguous float64 [5][1] inputs and [8][1] outputs")
+        self.add_addresses(e, values.ctypes.data, out.ctypes.data, owner)
+        self.keep.append((values, out))
+
+    def add_addresses(self, e: GlacierEngine, src_addr: int, dst_addr: int, owner=None) -> None:
+        """add() for a caller that owns fixed, checked blocks (the BMI's input
+        and output blocks) and passes their addresses."""
+        _frame, uptr, rec = e._next_uniform()
+        self.engines.append(e)
+        self.h.append(e.h.value)
+        self.src.append(src_addr)
+        self.u.append(uptr)
+        self.dst.append(dst_addr)
+        self.keep.append(rec)
+        self.owners.append(owner)
+        e.step_index += 1
+
+    def run(self) -> None:
+        """The queued steps, in one synchronous call.  On an error no step has
+        run and the engines' step counters are rolled back."""
+        m = len(self.h)
+        if m == 0:
+            return
+        arr = ctypes.c_void_p * m
+        engines = self.engines
+        try:
+            nat.check(engines[0].lib.tfg_update_many(arr(*self.h), m, arr(*self.src), arr(*self.u), arr(*self.dst)))
+        except Exception:
+            for e in engines:
+                e.step_index -= 1
+            raise
+        finally:
+            self.engines, self.h, self.src, self.u, self.dst, self.keep, self.owners = [], [], [], [], [], [], []
+
+
+def update_many(engines, values, outs) -> None:
+    """One step of each one-cell fp64 engine in ONE launch (tfg_update_many):
+    for engine i, the same as ``engines[i].update_io(values[i], outs[i])``
+    and bit for bit the same result.  values[i] [5][1] and outs[i] [8][1] are
+    C-contiguous float64 host arrays, read and filled by the call.  The engines
+    share one device and one stream (the BMI's tfg_shared_stream); each appears
+    once."""
+    b = UpdateBatch()
+    for e, v, o in zip(engines, values, outs):
+        b.add(e, v, o)
+    b.run()
