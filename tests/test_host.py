@@ -310,3 +310,56 @@ def test_bmi_one_cell_path_does_not_need_torch():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert r.stdout.startswith("native-error") or r.stdout.startswith("ok"), r.stdout
+
+
+def test_update_batch_passes_each_queued_step_and_rolls_back_on_error():
+    """engine.UpdateBatch / BMI flush_updates without a GPU (a stand-in library
+    in place of tfg_update_many): the call gets every queued engine's handle,
+    input, uniform and output addresses in queue order; on an error no step
+    counts, the engines' step counters and the BMI clocks roll back, and every
+    batch has been taken off the queue."""
+    import ctypes
+    import types
+
+    from topoflow_glacier import _native as nat
+    from topoflow_glacier.bmi import bmi_topoflow_glacier as B
+    from topoflow_glacier.engine import UpdateBatch
+
+    calls = []
+
+    class Lib:
+        rc = nat.OK
+
+        def tfg_update_many(self, hs, m, src, u, dst):
+            calls.append([[a[i] for i in range(m)] for a in (hs, src, u, dst)])
+            return self.rc
+
+    lib = Lib()
+
+    class Eng:
+        n, dtype_code = 1, nat.F64
+
+        def __init__(self, h):
+            self.h, self.lib, self.step_index = ctypes.c_void_p(h), lib, 7
+
+        def _next_uniform(self):
+            return 0, 9000 + self.h.value, None
+
+    e1, e2 = Eng(100), Eng(200)
+    b = UpdateBatch()
+    b.add_addresses(e1, 11, 21)
+    b.add_addresses(e2, 12, 22)
+    assert len(b) == 2 and (e1.step_index, e2.step_index) == (8, 8)
+    b.run()
+    assert calls[-1] == [[100, 200], [11, 12], [9100, 9200], [21, 22]] and len(b) == 0
+    lib.rc = nat.ERR_ARG
+    m1 = types.SimpleNamespace(_queued=True, _timestep=8)
+    b.add_addresses(e1, 11, 21, m1)
+    B._BATCHES[("dev", 0)] = b
+    with pytest.raises(nat.NativeError):
+        B.flush_updates()
+    assert e1.step_index == 8 and m1._timestep == 7 and not m1._queued and not B._BATCHES
+    B.flush_updates()  # nothing queued: no call
+    assert len(calls) == 2
+    with pytest.raises(ValueError):
+        UpdateBatch().add(e1, np.zeros(4), np.zeros(8))
