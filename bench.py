@@ -311,7 +311,10 @@ def main():
     backend = os.environ.get("TFG_BENCH_BACKEND", "nccl")
     if os.environ.get("TFG_BENCH_ONE_DEVICE") == "1":
         local = 0
-    if world > 1:
+    # TFG_BENCH_PG=1: a process group at world size 1 too, so the N > 1 barrier,
+    # max-over-ranks and diagnostics all-reduce run over RCCL on a one-GPU box
+    pg = world > 1 or os.environ.get("TFG_BENCH_PG") == "1"
+    if pg:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -336,7 +339,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize(local)
-        if world > 1:
+        if pg:
             dist.barrier()
 
     cond_ms = []
@@ -371,13 +374,13 @@ def main():
     elapsed = time.perf_counter() - t0
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
-    if world > 1:
+    if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     cells = rows * args.nx
     total_cells = ny_global * args.nx if args.scaling == "strong" else cells * world
     value = total_cells * steps / elapsed
-    diag = allreduce_diagnostics(eng.diagnostics()) if world > 1 else eng.diagnostics()
+    diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
 
     mean_launch_s = float(launch_ms.mean()) / 1e3
     bytes_launch = cells * launch_bytes_per_cell(args.fuse)
@@ -457,7 +460,7 @@ def main():
             "mass_balance": {k: float(v) for k, v in zip(["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"], diag[0])},
         }
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if pg:
         dist.barrier()
         dist.destroy_process_group()
     return result

@@ -85,3 +85,28 @@ def test_sharded_engine_gloo_world2(tmp_path):
     np.testing.assert_array_equal(red, ranks[1]["reduced"][0])
     assert _rel(red[:3], whole["diag_ref"][:3]) <= 1e-5
     assert red[5] == whole["diag_ref"][5] or _rel(red[5], whole["diag_ref"][5]) <= 1e-7
+
+
+@pytest.mark.gpu
+def test_rccl_paths_world1(tmp_path):
+    """RCCL (the nccl backend) on the one GPU of the test box, world size 1
+    (RCCL refuses two ranks on one device): the diagnostics all-reduce, a
+    batched point-to-point exchange of device tensors with the rank itself,
+    and the nccl branches of sharding.lateral_conduction and sharding.ice_flow
+    equal the same work without a process group, bit for bit."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", str(ROOT / "tests" / "rccl_worker.py"), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    z = dict(np.load(tmp_path / "rank0.npz"))
+    assert str(z["backend"]) == "nccl"
+    np.testing.assert_array_equal(z["diag_out"], z["diag_in"])
+    if "p2p_refused" in z:
+        print("self point-to-point refused:", z["p2p_refused"])
+    else:
+        np.testing.assert_array_equal(z["p2p_received"], z["p2p_sent"])
+    np.testing.assert_array_equal(z["qc_rccl"], z["qc_local"])
+    assert np.any(z["qc_local"] != 0)
+    assert int(z["nsub_rccl"]) == int(z["nsub_local"]) >= 1
+    np.testing.assert_array_equal(z["iwe_rccl"], z["iwe_local"])
