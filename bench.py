@@ -208,9 +208,15 @@ def cpu_baseline(args, run_gpu_sample):
         flip, genuine = melt_out_flips(gpu, ref)
         ok = valid_mask(flip, ps)
         err = max(_floored_rel(g[ok], ref[k][ok])[0] for k, g in gpu.items())
+        pure = {}  # the fraction of compared values above pure-relative 1e-5
+        for k, g in gpu.items():
+            gv, rv = g[ok].astype(np.float64), ref[k][ok]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
+            pure[k] = float(np.mean(rel > 1e-5))
         rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
         parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "cells": pn, "steps": ps,
-                  "outputs": names, "max_floored_rel": err, "tolerance": 1e-5,
+                  "outputs": names, "max_floored_rel": err, "tolerance": 1e-5, "frac_above_pure_rel_1e-5": pure,
                   "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"],
                   "flip_ratio": rule["ratio"], "flip_budget": rule["budget"], "flip_rule": rule["rule"],
                   "genuine_mismatches": len(genuine), "fp64_baseline_genuine_mismatches": len(genuine64),
