@@ -188,6 +188,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
   }
 }
 
+#ifndef TFG_PARAM_RELOAD
+#define TFG_PARAM_RELOAD 1  // k_fused re-reads the model constants every step (see advance)
+#endif
 #ifndef TFG_MIN_WAVES
 #define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
 #endif
@@ -338,6 +341,17 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
         f.q[0] = sload(ring + (int64_t)un->slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u));
       };
       auto advance = [&](int k, const Frame& f) {
+#if TFG_PARAM_RELOAD
+        // The model constants re-read from the kernel-argument segment every
+        // step (scalar loads, scalar cache hits) instead of being held for the
+        // whole launch, which spills them to VGPR lanes and reads each back
+        // with a v_readlane (a VALU instruction) at every use.  SGPR spills
+        // 62 -> 56 (fp32) and 170 -> 111 (fp64); same-box A/B: fp32 -0.6 %
+        // and fp64 -3.4 % time per launch.
+        auto pk = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(pk));
+        const DevParams& p = *(const DevParams*)pk;
+#endif
         const tfg_uniforms* up = uni + k;
         const tfg_uniforms u = *up;
         int32_t qn[C];
