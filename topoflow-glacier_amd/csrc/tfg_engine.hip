@@ -82,6 +82,25 @@ struct KArgs {
   uint32_t io_seq;
 };
 
+// TFG_STEP_PARAMS(p): inside a step loop, `p` names the launch's model
+// constants (KArgs::p, at offset 0 of the kernel-argument segment) through a
+// pointer an empty asm re-defines every step.  The compiler then re-issues
+// them as scalar loads (scalar cache hits) each step instead of holding them
+// for the whole launch, which spills them to VGPR lanes and reads each back
+// with a v_readlane (a VALU instruction) at every use.
+static_assert(offsetof(KArgs, p) == 0, "KArgs::p is read at the start of the kernel-argument segment");
+#ifndef TFG_PARAM_RELOAD
+#define TFG_PARAM_RELOAD 1  // k_fused and k_cell_run re-read the model constants every step
+#endif
+#if TFG_PARAM_RELOAD
+#define TFG_STEP_PARAMS(p)                                                                                  \
+  auto p##_ks = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr(); \
+  asm volatile("" : "+s"(p##_ks));                                                                          \
+  const DevParams& p = *(const DevParams*)p##_ks
+#else
+#define TFG_STEP_PARAMS(p) const DevParams& p = a.p
+#endif
+
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
 template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
 
@@ -188,9 +207,6 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
   }
 }
 
-#ifndef TFG_PARAM_RELOAD
-#define TFG_PARAM_RELOAD 1  // k_fused re-reads the model constants every step (see advance)
-#endif
 #ifndef TFG_MIN_WAVES
 #define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
 #endif
@@ -341,17 +357,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
         f.q[0] = sload(ring + (int64_t)un->slot * n_pad, sizeof(R) == 4 ? oR : lane_off(lc * 4u));
       };
       auto advance = [&](int k, const Frame& f) {
-#if TFG_PARAM_RELOAD
-        // The model constants re-read from the kernel-argument segment every
-        // step (scalar loads, scalar cache hits) instead of being held for the
-        // whole launch, which spills them to VGPR lanes and reads each back
-        // with a v_readlane (a VALU instruction) at every use.  SGPR spills
-        // 62 -> 56 (fp32) and 170 -> 111 (fp64); same-box A/B: fp32 -0.6 %
-        // and fp64 -3.4 % time per launch.
-        auto pk = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(pk));
-        const DevParams& p = *(const DevParams*)pk;
-#endif
+        // SGPR spills 62 -> 56 (fp32) and 170 -> 111 (fp64); same-box A/B:
+        // fp32 -0.6 % and fp64 -3.4 % time per launch.
+        TFG_STEP_PARAMS(p);
         const tfg_uniforms* up = uni + k;
         const tfg_uniforms u = *up;
         int32_t qn[C];
@@ -684,6 +692,7 @@ __global__ __launch_bounds__(64 * tfg::kCellWaves) void k_cell_run(const KArgs a
   In cur, nxt;
   fetch(0, cur);
   for (int k = 0; k < a.K; ++k) {
+    TFG_STEP_PARAMS(p);  // per-step constants (-2.5 % per step, same-box A/B, scripts/gpu_ab_cellrun.sh)
     fetch(k + 1, nxt);
     const tfg_uniforms u = uni[k];
     CellOut o;
