@@ -19,7 +19,7 @@ per = defaultdict(list)
 
 def short(name):
     """kernel name without its parameter list: 'k_fused<float, false, false, false, 1>'"""
-    name = name.replace("void ", "", 1).replace("(anonymous namespace)::", "")
+    name = name.replace("void ", "", 1).replace("(anonymous namespace)::", "").replace("tfg_kern::", "")
     return name.split("(")[0][:120]
 
 

@@ -287,8 +287,7 @@ def test_library_is_built_from_these_sources():
 
     info = _native.load().tfg_build_info().decode()
     assert f"tfg-src-sha256={G.built_hash(G.LIB)}" in info
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-cuid=tfg_engine"]
-    assert G.built_hash(G.LIB) == G.source_hash(flags), "stale _tfg.so: run __graft_entry__.build()"
+    assert G.built_hash(G.LIB) == G.source_hash(G.build_flags()), "stale _tfg.so: run __graft_entry__.build()"
     assert _native.code_object_sha256() is not None
 
 
