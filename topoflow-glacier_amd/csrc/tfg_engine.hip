@@ -866,12 +866,20 @@ int tfg_abi_version(void) { return TFG_ABI_VERSION; }
 #define TFG_SRC_HASH "unknown"
 #endif
 // build() (__graft_entry__.py) passes the sha256 of the sources and flags; it
-// finds this string in the built library to decide whether to recompile.
+// finds this string in the built library to decide whether to recompile.  Host
+// side only: in the device code it would make the code objects (whose sha256
+// keys the PMC provenance in bench.py) change with every source edit.
+#define TFG_STR2(x) #x
+#define TFG_STR(x) TFG_STR2(x)
+#if !defined(__HIP_DEVICE_COMPILE__)
 __attribute__((used)) static const char tfg_build_tag[] =
-    "libtfg abi=4 arch=gfx950 (hipcc) tfg-src-sha256=" TFG_SRC_HASH
-    "; kernels: k_fused<float|double,exact|fast,...>, k_diag_reduce, k_fill_synthetic";
+    "libtfg abi=" TFG_STR(TFG_ABI_VERSION) " arch=gfx950 (hipcc) tfg-src-sha256=" TFG_SRC_HASH
+    "; kernels: k_fused<float|double,exact|fast,...>, k_cell, k_cell_run, k_cell_many, k_diag_reduce, k_fill_synthetic";
 
 const char* tfg_build_info(void) { return tfg_build_tag; }
+#else
+const char* tfg_build_info(void);
+#endif
 
 int tfg_device_count(int* count) {
   if (!count) return fail(nullptr, TFG_ERR_ARG, "null count");
