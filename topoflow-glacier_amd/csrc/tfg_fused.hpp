@@ -81,6 +81,20 @@ static_assert(offsetof(KArgs, p) == 0, "KArgs::p is read at the start of the ker
 #define TFG_STEP_PARAMS(p) const DevParams& p = a.p
 #endif
 
+// The constants re-read at each phase of the fp64 step (TFG_EXACT_PHASES):
+// each call re-defines the kernel-argument pointer, so a phase's scalar loads
+// cannot be hoisted into an earlier phase.
+#ifndef TFG_EXACT_PHASES
+#define TFG_EXACT_PHASES 0
+#endif
+struct KernargParams {
+  __device__ const DevParams& operator()() const {
+    auto k = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return *(const DevParams*)k;
+  }
+};
+
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
 template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
 
@@ -350,8 +364,13 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
             CellOut o;
             CellDiag& d = CATCH ? cacc[j] : acc;
             const bool valid = (c0 + j) < a.n;
+#if TFG_EXACT_PHASES
+            const KernargParams params;
+#else
+            const tfg::ParamsAsIs params{p};
+#endif
             tfg::cell_step_exact<QC>(p, SX[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
-                                     (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid, (double)qc[j]);
+                                     (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid, (double)qc[j], params);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           } else {

@@ -276,11 +276,19 @@ __device__ __forceinline__ double opaque(double v) {
 // ---------------------------------------------------------------------------
 // QC: add the cell's lateral conduction flux qc [W m-2] (tfg_conduction.hpp)
 // in the reference's Qc position of Q_sum (:1314); without it Qc = 0.
-template <bool QC>
+// The model constants as the caller holds them (ParamsAsIs), or re-read at
+// each phase of the step (the grid kernel's KernargParams, tfg_fused.hpp), so
+// that a phase's constants are live only in that phase.
+struct ParamsAsIs {
+  const DevParams& p;
+  __device__ const DevParams& operator()() const { return p; }
+};
+
+template <bool QC, class PS>
 __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
                                        double P, double T_air, double Hum_sp, double P_air, double uz,
                                        int32_t q_old, int32_t& q_new, CellState& st, CellOut& o,
-                                       CellDiag& d, bool valid, double qc) {
+                                       CellDiag& d, bool valid, double qc, const PS& params) {
 #pragma clang fp contract(off)
   const double dt = p.dt;
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
@@ -344,37 +352,39 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
   st.tot_q += (int64_t)q_new - (int64_t)q_old;
   const double albedo = albedo_step(p, st, st.tot_q >= p.thr_q, T_air);
+  const DevParams& p2 = params();  // Clear_Sky_Radiation phase
   // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
-  const double tau = npmin(npmax(exp(a_sa + (b_sa * u.m_opt)) - p.dust, 0.0), 1.0);
+  const double tau = npmin(npmax(exp(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
   double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos(u.omega_th + s.dlon) + s.sin_leq * u.sin_d);
   K_ET = npmax(K_ET, 0.0);
   const double a_s = -0.0363 - (0.0084 * W_p);
   const double b_s = -0.0572 - (0.0173 * W_p);
-  const double gam_s = (1.0 - exp(a_s + (b_s * u.m_opt))) + p.dust;
+  const double gam_s = (1.0 - exp(a_s + (b_s * u.m_opt))) + p2.dust;
   const double K_dif = 0.5 * gam_s * u.k_et_flat;
   const double K_global = tau * u.k_et_flat + K_dif;
   const double K_bs = 0.5 * gam_s * albedo * K_global;
   double K_cs = (tau * K_ET) + K_dif + K_bs;
   double T_sr, T_ss;
-  slope_sun_offsets(p, s, u.tan_d, u.flat_sr, u.flat_ss, T_sr, T_ss);
+  slope_sun_offsets(p2, s, u.tan_d, u.flat_sr, u.flat_ss, T_sr, T_ss);
   if ((u.th <= T_sr) || (u.th >= T_ss)) K_cs = 0.0;
   const double Qn_SW = K_cs * (1.0 - albedo);  // :1139
+  const DevParams& p3 = params();  // long-wave and net flux phase
   // update_em_air :1167-1192
   const double T_air_K = T_air + 273.15;
   double em_air;
-  if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * pow((e_air / 10.0) / T_air_K, p.one_seventh);
-    em_air = (term1 * p.cloud_term) + p.F;
+  if (!p3.satterlund) {
+    const double term1 = p3.one_minus_F_172 * pow((e_air / 10.0) / T_air_K, p3.one_seventh);
+    em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
     em_air = 1.08 * (1.0 - exp(-1.0 * pow(e_air, T_air_K / 2016.0)));
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
-  const double LW_in = em_air * p.sigma * pow(T_air_K, opaque(4.0));
-  double LW_out = p.em_surf_sigma * pow(T_surf_K, opaque(4.0));
-  LW_out = LW_out + p.one_minus_em_surf * LW_in;
+  const double LW_in = em_air * p3.sigma * pow(T_air_K, opaque(4.0));
+  double LW_out = p3.em_surf_sigma * pow(T_surf_K, opaque(4.0));
+  LW_out = LW_out + p3.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
   // :1314 (Qa = 0; Qc = 0 unless the optional conduction term is on)
   const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + (QC ? qc : 0.0);
@@ -384,7 +394,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
            ((0.00391838 * pow(RH, opaque(1.5))) * atan(0.023101 * RH)) - 4.86035;
   }
-  melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
+  const DevParams& p4 = params();  // melt and mass phase
+  melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
   { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_ET, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
 #endif
