@@ -444,7 +444,8 @@ class UpdateBatch:
     """Single steps of one-cell fp64 engines that share a device and a stream,
     queued by :meth:`add` and run together by :meth:`run`: one
     tfg_update_many call, one launch (k_cell_many), the results of as many
-    ``update_io`` calls bit for bit.  An engine may be queued once per run."""
+    ``update_io`` calls bit for bit.  An engine may be queued once per run,
+    and must not be closed while queued (the BMI flushes before finalize)."""
 
     __slots__ = ("engines", "h", "src", "u", "dst", "keep", "owners")
 
