@@ -260,15 +260,29 @@ __device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st,
 }
 
 // A value the compiler cannot see as a constant.  pow() calls with a constant
-// exponent (T^4, RH^1.5) or base (10^y) go through it, so that the compiler
-// emits the general pow in every kernel: the library's call-simplification
-// may otherwise rewrite pow(x, 4.0) as multiplications in one kernel and not
-// in another, and the one-cell step (cell_step_exact_wave, whose exponents are
-// per-lane values) would no longer equal the grid step bit for bit.  numpy's
-// `** 4.0` is the general pow too.
+// base (Satterlund's 10^y) go through it, so that the compiler emits the
+// general pow in every kernel: the library's call-simplification may otherwise
+// rewrite such a call in one kernel and not in another, and the one-cell step
+// (cell_step_exact_wave, whose pow arguments are per-lane values) would no
+// longer equal the grid step bit for bit.
 __device__ __forceinline__ double opaque(double v) {
   asm volatile("" : "+v"(v));
   return v;
+}
+
+// x^4 and x^1.5 of the exact engine (T^4 in the long-wave terms, :1231-1233;
+// RH^1.5 of the wet bulb, :1520) as (x*x)*(x*x) and x*sqrt(x) instead of the
+// general pow: at most ~1.5 ulp from numpy's correctly rounded `** 4.0` /
+// `** 1.5`, against ~130 VALU instructions per general fp64 pow.  Grid and
+// one-cell steps both call these, so they stay equal bit for bit.
+__device__ __forceinline__ double pow4(double x) {
+#pragma clang fp contract(off)
+  const double x2 = x * x;
+  return x2 * x2;
+}
+__device__ __forceinline__ double pow1p5(double x) {
+#pragma clang fp contract(off)
+  return x * __builtin_sqrt(x);
 }
 
 // ---------------------------------------------------------------------------
@@ -382,8 +396,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
-  const double LW_in = em_air * p3.sigma * pow(T_air_K, opaque(4.0));
-  double LW_out = p3.em_surf_sigma * pow(T_surf_K, opaque(4.0));
+  const double LW_in = em_air * p3.sigma * pow4(T_air_K);
+  double LW_out = p3.em_surf_sigma * pow4(T_surf_K);
   LW_out = LW_out + p3.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
   // :1314 (Qa = 0; Qc = 0 unless the optional conduction term is on)
@@ -392,7 +406,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   double T_wb = 0.0;
   if (P_snow > 0.0) {
     T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
-           ((0.00391838 * pow(RH, opaque(1.5))) * atan(0.023101 * RH)) - 4.86035;
+           ((0.00391838 * pow1p5(RH)) * atan(0.023101 * RH)) - 4.86035;
   }
   const DevParams& p4 = params();  // melt and mass phase
   melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
@@ -409,11 +423,11 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
 // one function run once, lane i evaluating the i-th argument.  With W = 4
 // waves (one per SIMD of the CU), the function classes of a level also run
 // side by side, wave c taking class c (level 1: pow | exp | log | cos, acos;
-// level 2: pow | exp | atan; level 3: exp), and their results meet in LDS
+// level 2: exp | atan, and Satterlund's pow; level 3: exp), and their results meet in LDS
 // behind one barrier per level; with W = 1 the classes run one after another
 // in the wave and the results are read back from their lanes (v_readlane).
-// The serial chain of fp64 libm calls falls from 14-22 (exp x7, log x2,
-// pow x3-4, cos, acos, atan x4 where it snows) to 3 levels.  The same
+// The serial chain of fp64 libm calls falls from 13-19 (exp x7, log x2,
+// pow x1, cos, acos, atan x4 where it snows) to 3 levels.  The same
 // functions on the same arguments give the same values, so the result equals
 // cell_step_exact bit for bit (test_one_cell_kernels_equal_the_grid_kernel).
 // ---------------------------------------------------------------------------
@@ -488,12 +502,12 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   }
   if (X.mine(X_POW1)) {
     double px, py;
-    if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167), T_a^4 (:1231)
-      px = lane == 1 ? T_air_K : (e_air / 10.0) / T_air_K;
-      py = lane == 1 ? 4.0 : p.one_seventh;
-    } else {              // e_air^(T/2016) (:1190), T_a^4, 10^(...) of e_sat_air (:796)
-      px = lane == 1 ? T_air_K : (lane == 2 ? 10.0 : e_air);
-      py = lane == 1 ? 4.0 : (lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
+    if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167)
+      px = (e_air / 10.0) / T_air_K;
+      py = p.one_seventh;
+    } else {              // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
+      px = lane == 2 ? 10.0 : e_air;
+      py = lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0;
     }
     pw1 = pow(px, py);
   }
@@ -504,7 +518,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (W > 1) lds_level_barrier();
   const double e_p0 = X.get(X_EXP1, ex1, 0), e_es = X.get(X_EXP1, ex1, 1), e_alb = X.get(X_EXP1, ex1, 2);
   const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1);
-  const double pw_em = X.get(X_POW1, pw1, 0), pw_ta4 = X.get(X_POW1, pw1, 1), pw_es = X.get(X_POW1, pw1, 2);
+  const double pw_em = X.get(X_POW1, pw1, 0), pw_es = X.get(X_POW1, pw1, 2);
+  const double pw_ta4 = pow4(T_air_K);  // :1231
   if (W > 1) {
     cos_wl = X.get(X_TRIG1, 0.0, 0);
     ac = X.get(X_TRIG1, 0.0, 1);
@@ -548,11 +563,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
     ex2 = exp(ea2);
   }
-  if (X.mine(X_POW2)) {
-    double qx = lane == 1 ? RH : T_surf_K, qy = lane == 1 ? 1.5 : 4.0;             // :1520, :1233
-    if (p.satterlund && lane == 2) { qx = 10.0; qy = 11.4 - 2353.0 / (T_surf + 273.15); }  // :796 (surface)
-    pw2 = pow(qx, qy);
-  }
+  if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15));  // :796 (surface)
   if (X.mine(X_ATAN2) && P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
     at2 = atan(lane == 1 ? T_air + RH : (lane == 2 ? RH - 1.676331 : (lane == 3 ? 0.023101 * RH
                                                                                  : 0.151977 * sqrt(RH + 8.313659))));
@@ -560,7 +571,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   X.put(X_POW2, pw2);
   X.put(X_ATAN2, at2);
   if (W > 1) lds_level_barrier();
-  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : X.get(X_POW2, pw2, 2) / 1000.0;
+  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : X.get(X_POW2, pw2, 0) / 1000.0;
   e_sat_surf = e_sat_surf * 10.0;
   const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
@@ -595,7 +606,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
   }
   const double LW_in = em_air * p.sigma * pw_ta4;
-  double LW_out = p.em_surf_sigma * X.get(X_POW2, pw2, 0);
+  double LW_out = p.em_surf_sigma * pow4(T_surf_K);  // :1233
   LW_out = LW_out + p.one_minus_em_surf * LW_in;
   const double Qn_LW = LW_in - LW_out;
   // :1314 (Qa = 0; qc = 0 unless the optional conduction term is on)
@@ -603,7 +614,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   double T_wb = 0.0;
   if (P_snow > 0.0) {
     T_wb = T_air * X.get(X_ATAN2, at2, 0) + X.get(X_ATAN2, at2, 1) - X.get(X_ATAN2, at2, 2) +
-           ((0.00391838 * X.get(X_POW2, pw2, 1)) * X.get(X_ATAN2, at2, 3)) - 4.86035;
+           ((0.00391838 * pow1p5(RH)) * X.get(X_ATAN2, at2, 3)) - 4.86035;
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
