@@ -75,6 +75,12 @@ def auto_fuse(cells: int) -> int:
     return FUSE_BIG if cells > FUSE_SPLIT_CELLS else FUSE_SMALL
 
 
+def warmup_steps(requested: int, fuse: int) -> int:
+    """Untimed steps before the timed region: the requested count, and at
+    least one whole launch of the timed depth (main() says why)."""
+    return max(requested, fuse)
+
+
 def timed_steps(requested: int, fuse: int, explicit: bool) -> int:
     """Whole launches covering `requested`, at least MIN_LAUNCHES of them.  With
     the automatic depth the count is a multiple of STEP_QUANTUM and at least
@@ -359,8 +365,13 @@ def main():
         lateral_conduction(eng, cfg.k_snow, cfg.k_ice, 30.0, 30.0, distributed=world > 1)
         cond_ms.append((time.perf_counter() - t) * 1e3)
 
-    # warmup (untimed)
-    eng.run(args.warmup)
+    # warmup (untimed): the requested steps, and at least one whole launch of
+    # the timed depth.  The first full-depth launch after a short warm-up runs
+    # 10-29 ms long on 8192/N-row slabs (scripts/gpu_slab_warmup.sh,
+    # profiles/r2p_slab_warmup.json: 1024 x 8192 after --warmup 5: 43.3 ms, then
+    # 14.8 and 14.3 ms); after one such launch every later one is steady.
+    warm_steps = warmup_steps(args.warmup, args.fuse)
+    eng.run(warm_steps)
     barrier()
     # Whole fused launches, and at least MIN_LAUNCHES of them, so that a short
     # --steps still gives a multi-launch timed region; the JSON carries the
@@ -429,8 +440,10 @@ def main():
                 + ("" if fuse_explicit else f", and a multiple of {STEP_QUANTUM} steps so that every GPU count "
                                             f"times the same work")),
             "launches": {"count": n_launch, "steps_each": args.fuse, "ms_min": float(launch_ms.min()),
-                         "ms_mean": float(launch_ms.mean()), "ms_max": float(launch_ms.max())},
+                         "ms_mean": float(launch_ms.mean()), "ms_max": float(launch_ms.max()),
+                         "ms_each": [round(float(x), 3) for x in launch_ms]},
             "warmup": args.warmup,
+            "warmup_steps_run": warm_steps,
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
             "scaling": args.scaling,

@@ -47,6 +47,8 @@ def test_driver_command_times_the_same_work_at_every_n(world, fuse):
     steps = bench.timed_steps(args.steps, k, explicit=False)
     assert k == fuse and steps == 576 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
     assert bench.timed_steps(48, 24, explicit=True) == 72  # an explicit --fuse: >= 3 launches of it
+    # the driver's --warmup 5 still warms one whole launch of the timed depth
+    assert bench.warmup_steps(args.warmup, k) == k and bench.warmup_steps(400, k) == 400
 
 
 def test_weak_scaling_stays_behind_its_flag():
