@@ -470,6 +470,10 @@ def main():
                 "traffic_source": traffic_source,
                 "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
                 "kernel_ms_per_launch": float(launch_ms.mean()),
+                "note": None if args.engine == "float32" else (
+                    "the fp64 engine is compute-bound, not HBM-bound: its step issues 1536 VALU instructions per "
+                    "wave and cell-step, 89 % of the vector pipe at 4 waves per SIMD (profiles/r2p_issue_counters.json); "
+                    "frac is its HBM share only"),
             },
             "cpu_baseline": cpu,
             "cpu_baseline_numpy_1core": numpy_leg,
