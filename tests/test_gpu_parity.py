@@ -168,8 +168,11 @@ def test_fp64_engine_vs_reference_fixtures(name):
     rule = flip_rule(int((flip >= 0).sum()), fp64_baseline_flips(c64, g["outputs"], 1e-10))
     assert rule["ok"], rule
     mask = valid_mask(flip, g["nsteps"])
+    errs = {v: float(parity(outs[v], g["outputs"][v], mask=mask)[0]) for v in HIST}
+    _report(f"fp64_fixture_{name}", {"max_rel_by_output": errs, "melt_out_flips": rule["flips"],
+                                     "fp64_baseline_flips": rule["fp64_flips"]})
     for v in HIST:
-        assert parity(outs[v], g["outputs"][v], mask=mask)[0] <= 1e-10, v
+        assert errs[v] <= 1e-10, v
     keep = flip < 0
     assert parity(state["h_swe"], g["outputs"]["h_swe"][-1], mask=keep)[0] <= 1e-10
     assert parity(state["h_iwe"], g["outputs"]["h_iwe"][-1], mask=keep)[0] <= 1e-10
