@@ -284,6 +284,16 @@ __device__ __forceinline__ double pow1p5(double x) {
 #pragma clang fp contract(off)
   return x * __builtin_sqrt(x);
 }
+// em_air's (e/T)^(1/7) (:1167) as exp(log(x)/7): x is ~2e-3, so the log's
+// rounding moves the exponent by ~1e-16 and the result stays within ~3 ulp of
+// numpy's pow, while the general pow's extra-precision log and special cases
+// cost about twice the log + exp pair.  The one-cell step batches the log with
+// level 1's logs and the exp with level 2's exps, which leaves no general pow
+// in its chain unless SATTERLUND is set.
+__device__ __forceinline__ double pow_small_root(double x, double inv_n) {
+#pragma clang fp contract(off)
+  return exp(log(x) * inv_n);
+}
 
 // ---------------------------------------------------------------------------
 // EXACT variant (fp64, reference order)
@@ -389,7 +399,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * pow((e_air / 10.0) / T_air_K, p3.one_seventh);
+    const double term1 = p3.one_minus_F_172 * pow_small_root((e_air / 10.0) / T_air_K, p3.one_seventh);
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
     em_air = 1.08 * (1.0 - exp(-1.0 * pow(e_air, T_air_K / 2016.0)));
@@ -422,12 +432,12 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
 // transcendental calls are batched by dependency level: each level's calls of
 // one function run once, lane i evaluating the i-th argument.  With W = 4
 // waves (one per SIMD of the CU), the function classes of a level also run
-// side by side, wave c taking class c (level 1: pow | exp | log | cos, acos;
-// level 2: exp | atan, and Satterlund's pow; level 3: exp), and their results meet in LDS
+// side by side, wave c taking class c (level 1: exp | log | cos, acos, and
+// Satterlund's pow; level 2: exp | atan, and Satterlund's pow; level 3: exp), and their results meet in LDS
 // behind one barrier per level; with W = 1 the classes run one after another
 // in the wave and the results are read back from their lanes (v_readlane).
-// The serial chain of fp64 libm calls falls from 13-19 (exp x7, log x2,
-// pow x1, cos, acos, atan x4 where it snows) to 3 levels.  The same
+// The serial chain of fp64 libm calls falls from 14-18 (exp x8, log x3,
+// cos, acos, atan x4 where it snows) to 3 levels.  The same
 // functions on the same arguments give the same values, so the result equals
 // cell_step_exact bit for bit (test_one_cell_kernels_equal_the_grid_kernel).
 // ---------------------------------------------------------------------------
@@ -495,29 +505,21 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const double x_alb = -st.n * r_alb;                          // :1041
     ex1 = exp(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
-  if (X.mine(X_LOG1)) lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : e_air / 6.1121);  // :670, :888
+  if (X.mine(X_LOG1))  // :670, :888, and em_air's root (:1167, pow_small_root)
+    lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : (lane == 2 ? (e_air / 10.0) / T_air_K : e_air / 6.1121));
   if (X.mine(X_TRIG1)) {
     cos_wl = cos(u.omega_th + s.dlon);                                        // SF:867 (one argument)
     ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));            // SF:325 (one argument)
   }
-  if (X.mine(X_POW1)) {
-    double px, py;
-    if (!p.satterlund) {  // em_air's (e/T)^(1/7) (:1167)
-      px = (e_air / 10.0) / T_air_K;
-      py = p.one_seventh;
-    } else {              // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
-      px = lane == 2 ? 10.0 : e_air;
-      py = lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0;
-    }
-    pw1 = pow(px, py);
-  }
+  if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
+    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
   X.put(X_EXP1, ex1);
   X.put(X_LOG1, lg1);
   X.put(X_TRIG1, lane == 1 ? ac : cos_wl);
   X.put(X_POW1, pw1);
   if (W > 1) lds_level_barrier();
   const double e_p0 = X.get(X_EXP1, ex1, 0), e_es = X.get(X_EXP1, ex1, 1), e_alb = X.get(X_EXP1, ex1, 2);
-  const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1);
+  const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1), log_em = X.get(X_LOG1, lg1, 2);
   const double pw_em = X.get(X_POW1, pw1, 0), pw_es = X.get(X_POW1, pw1, 2);
   const double pw_ta4 = pow4(T_air_K);  // :1231
   if (W > 1) {
@@ -561,6 +563,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (X.mine(X_EXP2)) {
     double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
     if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
+    if (lane == 3) ea2 = log_em * p.one_seventh;                                    // :1167 (pow_small_root)
     ex2 = exp(ea2);
   }
   if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15));  // :796 (surface)
@@ -600,7 +603,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :1167-1192, :1231-1248
   double em_air;
   if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * pw_em;
+    const double term1 = p.one_minus_F_172 * X.get(X_EXP2, ex2, 3);
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
