@@ -251,22 +251,50 @@ def shard_plan(args, world: int, rank: int) -> dict:
 def pmc_traffic(rows, args):
     """HBM bytes per launch from the committed PMC profile of this shard shape
     (scripts/gpu_pmc.sh -> profiles/pmc_<nx>x<rows>_fuse<K>.json), quoted only
-    when the profile was measured on device code identical to the running
-    library's (sha256 of its .hip_fatbin section); otherwise null, with the reason."""
+    when the profile was measured on the same machine code of the timed kernel
+    as the running library's (_native.kernel_code_sha256: the kernel's
+    instructions, descriptor and callees, not the other kernels of the
+    library); otherwise null, with the reason."""
     from topoflow_glacier import _native as nat
 
     pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}.json"
-    running = nat.code_object_sha256()
+    running = nat.kernel_code_sha256()
     if args.engine != "float32" or args.catchments or args.dt != 1.0 or args.conduction:
         return None, {"profile": None, "reason": "no PMC profile for this variant of the kernel"}
     if not pmc.exists():
         return None, {"profile": None, "reason": f"{pmc.relative_to(ROOT)} not measured"}
     prof = json.loads(pmc.read_text())
-    measured = prof.get("code_object_sha256")
-    src = {"profile": str(pmc.relative_to(ROOT)), "code_object_sha256": measured,
-           "running_code_object_sha256": running, "match": measured is not None and measured == running,
+    measured = prof.get("kernel_code_sha256")
+    src = {"profile": str(pmc.relative_to(ROOT)), "kernel": nat.BENCH_KERNEL, "kernel_code_sha256": measured,
+           "running_kernel_code_sha256": running, "match": measured is not None and measured == running,
            "read_scale": corr.get("read_scale") if isinstance(corr := prof.get("correction"), dict) else None}
     return (prof.get("hbm_bytes_per_launch") if src["match"] else None), src
+
+
+def device_record(torch, local: int) -> dict:
+    """The GPU this rank drives: its PCI address (hipDeviceProp_t
+    pciDomainID:pciBusID:pciDeviceID, through torch.cuda.get_device_properties)
+    and UUID, so a multi-GPU line shows which physical devices ran."""
+    p = torch.cuda.get_device_properties(local)
+    return {"device": local, "pci_bus_id": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}",
+            "uuid": str(p.uuid), "name": p.name}
+
+
+def rank_report(records: list[dict], backend: str | None) -> dict:
+    """What every rank saw, gathered on rank 0: one record per rank (rank,
+    local_rank, device, PCI bus id, its launch times and its own timed span),
+    the slowest and fastest rank, and whether the ranks drove distinct GPUs.
+    Over RCCL two ranks on one GPU are an error (RCCL itself refuses them);
+    the gloo rehearsal on one device (TFG_BENCH_ONE_DEVICE) shares one."""
+    recs = sorted(records, key=lambda r: r["rank"])
+    span = [r["elapsed_s"] for r in recs]
+    buses = [r["pci_bus_id"] for r in recs]
+    distinct = len(set(buses)) == len(buses)
+    if backend == "nccl" and not distinct:
+        raise RuntimeError(f"RCCL ranks share a GPU: {buses}")
+    slow = max(range(len(recs)), key=lambda i: span[i])
+    return {"ranks": recs, "distinct_gpus": distinct, "n_distinct_gpus": len(set(buses)),
+            "slowest_rank": recs[slow]["rank"], "rank_time_max_over_min": max(span) / min(span)}
 
 
 def catchment_blocks(row0, rows, ny_global, nx, k):
@@ -390,6 +418,14 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    own = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **device_record(torch, local),
+           "row0": row0, "rows": rows, "elapsed_s": elapsed, "launch_ms_mean": float(launch_ms.mean()),
+           "launch_ms_min": float(launch_ms.min()), "launch_ms_max": float(launch_ms.max())}
+    records = [own]
+    if pg:
+        records = [None] * dist.get_world_size()
+        dist.all_gather_object(records, own)
+    ranks = rank_report(records, dist.get_backend() if pg else None)
     t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
     if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -431,6 +467,10 @@ def main():
             "value": value,
             "unit": "cell-updates/s",
             "n_gpus": world,
+            # what the process group saw (the driver's N > 1 lines): backend and
+            # size from torch.distributed itself, not the launcher's environment
+            "process_group": ({"backend": dist.get_backend(), "world_size": dist.get_world_size()} if pg else None),
+            "ranks": ranks,
             "steps": steps,
             "steps_requested": args.steps,
             "steps_note": None if steps == args.steps else (

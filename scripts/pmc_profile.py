@@ -9,9 +9,12 @@ profile bench.py quotes (profiles/pmc_<nx>x<ny>_fuse<K>.json).
   WRITE_SIZE scale for 4-byte lanes, the width k_fused uses.  The guide's
   gfx950 FETCH_SIZE x2 is calibrated for 16-byte lanes only
   (MI355X_MICROARCH.md, HBM/rocprofv3 section); this file records both.
-* code_object_sha256: the sha256 of the measured library's .hip_fatbin
-  section.  bench.py quotes `traffic` only when the running library's device
-  code has the same hash.
+* kernel_code_sha256: the sha256 of the measured kernel's own gfx950 machine
+  code (k_fused<float, false, false, false, false, 1>, its kernel descriptor
+  and the functions it calls; _native.kernel_code_sha256).  bench.py quotes
+  `traffic` only when the running library's kernel has the same hash, so edits
+  to other kernels leave the measurement valid.  code_object_sha256 (the whole
+  .hip_fatbin) is recorded beside it.
 """
 import csv
 import glob
@@ -22,7 +25,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "topoflow-glacier_amd"))
-from topoflow_glacier._native import code_object_sha256  # noqa: E402
+from topoflow_glacier._native import code_object_sha256, kernel_code_sha256  # noqa: E402
 
 sys.path.insert(0, str(ROOT))
 from bench import launch_bytes_per_cell  # noqa: E402  
@@ -81,6 +84,7 @@ def main():
         "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "
                    "calibration: rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE -- tools/hbm_mix 67108864 8 2048 0 cal); "
                    "python3 scripts/pmc_profile.py",
+        "kernel_code_sha256": kernel_code_sha256(),
         "code_object_sha256": code_object_sha256(),
         "correction": {
             "read_scale": rd_scale, "write_scale": wr_scale,
@@ -103,7 +107,7 @@ def main():
                                 if k.startswith("SQ_") and k != "SQ_WAVES"}
     out.write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps({k: res[k] for k in ("hbm_bytes_per_launch", "algorithmic_bytes_per_launch",
-                                          "traffic_over_algorithmic", "code_object_sha256")}))
+                                          "traffic_over_algorithmic", "kernel_code_sha256")}))
     print(json.dumps(cal, indent=1))
 
 

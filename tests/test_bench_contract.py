@@ -85,3 +85,45 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert sp["ok"] and sp["melt_out_flips"] <= sp["flip_budget"] and "flips_fp64_baseline" in sp
     ts = rf["traffic_source"]  # no PMC profile of this shape: traffic is null and says why
     assert rf["traffic"] is None and ts["reason"]
+
+
+def test_rank_report_names_the_devices_and_the_slowest_rank():
+    """The per-rank record a multi-GPU line carries (bench.rank_report): ranks
+    in order, the slowest one, max/min span, distinct GPUs; two RCCL ranks on
+    one GPU are refused (the one-device gloo rehearsal may share one)."""
+    bench, _ = _args()
+    rec = lambda r, bus, t: {"rank": r, "local_rank": r, "device": r, "pci_bus_id": bus, "elapsed_s": t}  # noqa: E731
+    rep = bench.rank_report([rec(1, "0000:15:00", 2.0), rec(0, "0000:05:00", 1.6)], "nccl")
+    assert [r["rank"] for r in rep["ranks"]] == [0, 1] and rep["slowest_rank"] == 1
+    assert rep["distinct_gpus"] and rep["n_distinct_gpus"] == 2 and rep["rank_time_max_over_min"] == 2.0 / 1.6
+    shared = [rec(0, "0000:05:00", 1.0), rec(1, "0000:05:00", 1.0)]
+    assert not bench.rank_report(shared, "gloo")["distinct_gpus"]
+    with pytest.raises(RuntimeError):
+        bench.rank_report(shared, "nccl")
+
+
+@pytest.mark.gpu
+def test_multi_rank_line_is_self_verifying():
+    """The N > 1 path, rehearsed on one GPU (two ranks over gloo, both on
+    cuda:0): the JSON names the process group's backend and size as
+    torch.distributed sees them and every rank's device, PCI bus id and launch
+    times, so a driver N = 2 / 4 / 8 line shows which GPUs ran and which rank
+    set the pace."""
+    import os
+
+    env = dict(os.environ, TFG_BENCH_ONE_DEVICE="1", TFG_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", "29531", str(ROOT / "bench.py"), "--gpus", "2", "--ny", "512", "--nx", "1024",
+           "--steps", "48", "--warmup", "24", "--fuse", "24"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["process_group"] == {"backend": "gloo", "world_size": 2}
+    rep = d["ranks"]
+    assert [x["rank"] for x in rep["ranks"]] == [0, 1] and rep["slowest_rank"] in (0, 1)
+    assert [x["rows"] for x in rep["ranks"]] == [256, 256] and rep["rank_time_max_over_min"] >= 1.0
+    for x in rep["ranks"]:
+        assert x["pci_bus_id"] and x["device"] == 0 and x["launch_ms_min"] <= x["launch_ms_mean"] <= x["launch_ms_max"]
+    assert rep["n_distinct_gpus"] == 1 and not rep["distinct_gpus"]  # both ranks on the one GPU of the box

@@ -1,8 +1,12 @@
 """Parity at the BASELINE.json GPU configurations' per-GPU sizes.
 
   * config 4 (the bench): 8192 x 8192, hourly, two 96-step launches (the
-    bench's shape, with the in-launch window reuse through LDS);
+    bench's launch shape: longer than the 72-slot window, so a launch reads
+    back window slots it wrote itself);
   * config 3: 4096 x 4096, hourly, two 24-step launches;
+  * config 2: 1024 x 1024, a year of hourly steps (8760) in 120-step launches,
+    the oracle's daily outputs on about 2048 sampled cells
+    (test_config2_year_at_its_own_shape);
   * config 5's per-GPU slab: rows 6144..8191 of the 16384 x 16384 grid over 8
     GPUs (2048 x 16384 cells), dt = 0.25 h (a 288-slot snowfall window), 43
     catchments (256 x 256-cell blocks, ids mod 43), 384 steps in four 96-step
@@ -34,7 +38,7 @@ SEED = 20251001
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
 CONFIGS = {
     # name: (ny, nx, row0, ny_global, dt, steps, fuse, catchments)
-    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 192, 96, 0),  # the bench's launch shape (window reuse in LDS)
+    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 192, 96, 0),  # the bench's launch shape
     "config3_4096sq": (4096, 4096, 0, 4096, 1.0, 48, 24, 0),
     "config5_slab_2048x16384_dt0.25_43catch": (2048, 16384, 6144, 16384, 0.25, 384, 96, 43),
 }
@@ -181,6 +185,114 @@ def test_full_size_sampled_parity_water_balance_and_determinism(name):
 
     # determinism: a second run, bit for bit
     gpu2, runoff2, _, _, swe2, dg2, _ = _run(torch, cfg, shape, cells, cid)
+    assert torch.equal(swe1, swe2) and np.array_equal(dg, dg2) and runoff == runoff2
+    for v in HIST:
+        assert np.array_equal(gpu[v], gpu2[v]), v
+
+
+# ---------------------------------------------------------------- config 2: a year at 1024 x 1024
+C2_NY = C2_NX = 1024
+C2_STEPS, C2_FUSE = 8760, 120  # 73 launches of 120 hourly steps
+
+
+def _run_year(torch, cfg, cells):
+    """Config 2 on the GPU: the whole 1024 x 1024 grid for a year of hourly
+    steps in 120-step launches.  Returns the sampled cells' outputs at the last
+    step of every day [365][ncell], the whole grid's runoff sum, storage sums
+    before and after, the final h_swe on device and the diagnostics."""
+    from topoflow_glacier.synthetic import diurnal_table
+
+    n = C2_NY * C2_NX
+    e = make_engine(cfg, C2_NY, C2_NX, "float32", n_frames=24, hist_depth=C2_FUSE, fuse_steps=C2_FUSE)
+
+    def dev(name, index, dtype):
+        return e.get_field_device(name, torch.empty(n, dtype=dtype, device="cuda:0"), index=index)
+
+    try:
+        e.fill_synthetic(SEED, diurnal_table(24), nx_global=C2_NX)
+        idx = torch.as_tensor(cells, device="cuda:0")
+        store0 = (float(dev("h_swe", 0, torch.float64).sum()), float(dev("h_iwe", 0, torch.float64).sum()))
+        daily = {v: [] for v in HIST}
+        runoff = torch.zeros((), dtype=torch.float64, device="cuda:0")
+        for launch in range(C2_STEPS // C2_FUSE):
+            e.run(C2_FUSE)
+            e.sync()
+            for k in range(C2_FUSE):
+                step = launch * C2_FUSE + k
+                runoff += dev("M_total", k, torch.float32).sum(dtype=torch.float64)
+                if step % 24 == 23:
+                    for v in HIST:
+                        daily[v].append(dev(v, k, torch.float32).index_select(0, idx).cpu().numpy())
+        swe1 = dev("h_swe", 0, torch.float64)
+        store1 = (float(swe1.sum()), float(dev("h_iwe", 0, torch.float64).sum()))
+        return ({v: np.stack(a).astype(np.float64) for v, a in daily.items()}, float(runoff), store0, store1, swe1,
+                e.diagnostics())
+    finally:
+        e.close()
+
+
+def test_config2_year_at_its_own_shape():
+    """BASELINE config 2 at its own shape: 1024 x 1024 cells, a year of hourly
+    steps (16384 waves, four rounds of the chip's resident waves per step).
+    Against the oracle's year on ~2048 sampled cells (the first and last cell,
+    both sides of every 2^k boundary, random others), compared once a day as
+    in test_fp32_free_run_over_a_year: snow depth within the floored 1e-5 and
+    RH within 1e-6 everywhere; SM outside 1e-5 (melt onset) in at most 0.5 %
+    of the cells; the cells whose ice melt switches at a different step (the
+    exact-zero melt-out gate, :1424) held to the flip rule against the fp64
+    baseline (the C oracle's year on the same cells); runoff diverging only
+    there or at melt onset.  Whole grid: water balance; determinism."""
+    import torch
+
+    import tfg_oracle as O
+    from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
+
+    cfg = dict(BASE_CFG)
+    n = C2_NY * C2_NX
+    cells = _sample_cells(np.random.default_rng(7), n, C2_NX)
+    gpu, runoff, s0, s1, swe1, dg = _run_year(torch, cfg, cells)
+
+    syn = synthetic_cells(SEED, cells, diurnal_table(24))
+    static = {k: np.asarray(syn[s], np.float64) for k, s in (("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"),
+              ("h0_snow", "h_snow"), ("h0_ice", "h_ice"), ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
+    m = O.OracleGrid(cfg, **static)
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], C2_STEPS, cfg["lon"])
+    ref = {v: [] for v in HIST}
+    for k in range(C2_STEPS):
+        f = k % 24
+        r = m.step(*(syn[v][f].astype(np.float64) for v in ("P", "T_air", "Hum_sp", "P_air", "uz")), jd[k], tsn[k])
+        if k % 24 == 23:
+            for v in HIST:
+                ref[v].append(np.array(r[v], copy=True))
+    ref = {v: np.stack(a) for v, a in ref.items()}
+    c = c_oracle_hist(cfg, static, {v: syn[v] for v in ("P", "T_air", "Hum_sp", "P_air", "uz")}, C2_STEPS,
+                      frames=np.arange(C2_STEPS) % 24, clock=(jd, tsn))
+    c_daily = {v: c[v][23::24] for v in HIST}
+
+    def diverged(A, v):
+        g, r = A[v], ref[v]
+        s_v = np.percentile(np.abs(r[r != 0]), 99) if np.any(r != 0) else 0.0
+        err = np.abs(g - r) / np.maximum(np.maximum(np.abs(r), s_v), 1e-300)
+        return float(err.max()), (err > 1e-5).any(axis=0)
+
+    assert diverged(gpu, "h_snow")[0] <= 1e-5
+    assert diverged(gpu, "RH")[0] <= 1e-6
+    assert diverged(gpu, "SM")[1].mean() <= 0.005
+    gi = diverged(gpu, "h_ice")[1] | diverged(gpu, "IM")[1]
+    ci = diverged(c_daily, "h_ice")[1] | diverged(c_daily, "IM")[1]
+    rule = flip_rule(int(gi.sum()), int(ci.sum()))
+    assert rule["ok"], rule
+    assert (diverged(gpu, "M_total")[1] & ~gi).mean() <= 0.005
+
+    # water balance over the whole grid: runoff = rain + snowfall + storage loss
+    da_m2 = BASE_CFG["da"] * 1e6
+    tot = dg.sum(axis=0)
+    lhs = runoff * cfg["dt"] * 3600 * da_m2
+    rhs = tot[1] + tot[2] + ((s0[0] - s1[0]) + (s0[1] - s1[1])) * da_m2
+    assert abs(lhs - rhs) <= 1e-5 * abs(rhs), (lhs, rhs)
+
+    # determinism: a second year, bit for bit
+    gpu2, runoff2, _, _, swe2, dg2 = _run_year(torch, cfg, cells)
     assert torch.equal(swe1, swe2) and np.array_equal(dg, dg2) and runoff == runoff2
     for v in HIST:
         assert np.array_equal(gpu[v], gpu2[v]), v

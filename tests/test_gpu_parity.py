@@ -562,28 +562,56 @@ def _report(name, obj):
             json.dump(obj, f, indent=1)
 
 
-def test_fp64_engine_propagates_nan_forcing_like_the_reference():
+@pytest.mark.parametrize("engine", ["float64", "float32"])
+def test_engine_propagates_nan_forcing_like_the_reference(engine):
     """Missing forcing (NaN) takes the same path as in the reference's numpy
-    arithmetic: np.maximum / np.minimum propagate NaN (:1364-1434), a NaN
-    snowfall poisons the window sum (:1040), so outputs turn NaN in the same
-    cells and steps and finite values still match.  (The fp32 engine uses IEEE
-    min/max and does not model missing data)"""
+    arithmetic, in both engines: np.maximum / np.minimum propagate NaN
+    (:906-910, :670, SF:614, SF:887, :1364-1434), P * (T > T_rs) and
+    P * (T <= T_rs) are both 0 for a NaN T_air (:585, :604), np.where leaves
+    Eccs alone for a NaN snowfall (:1537, :1558), and a NaN snowfall poisons
+    the 72-slot window sum (:1035-1041) so that the days since snowfall `n`
+    freeze until the slot leaves the window 72 steps later.  Outputs turn NaN
+    in the same cells and steps, finite values match (fp64: 1e-10 relative;
+    fp32 on the same fp32-rounded inputs: the floored 1e-5 of SURVEY 8(d)),
+    and so does the state, `n` included."""
     g = load_golden("grid64")
     cells = slice(8, 16)
-    forcing = {k: np.array(v[:40, cells], copy=True) for k, v in g["forcing"].items()}
-    static = {k: v[cells] for k, v in g["static"].items()}
+    nsteps = 100  # past step 5 + 72: the NaN slot leaves the window and n runs again
+    r32 = (lambda a: np.asarray(a, np.float32).astype(np.float64)) if engine == "float32" else np.asarray  # noqa: E731
+    forcing = {k: np.array(r32(v[:nsteps, cells]), copy=True) for k, v in g["forcing"].items()}
+    static = {k: r32(v[cells]) for k, v in g["static"].items()}
     forcing["T_air"][3, 0] = np.nan
+    forcing["P"][3, 0] = max(forcing["P"][3, 0], 2e-4)  # P with a NaN T_air: neither rain nor snow
     forcing["P"][5, 1] = np.nan
     forcing["Hum_sp"][2, 2] = np.nan
     forcing["uz"][7, 3] = np.nan
     forcing["P_air"][9, 4] = np.nan
-    outs, state, diag = gpu_run_fields(g["cfg"], static, forcing, 1, 8, "float64", 40)
+    outs, state, diag = gpu_run_fields(g["cfg"], static, forcing, 1, 8, engine, nsteps)
     ref, m = oracle_run(g["cfg"], static, forcing)
+    assert np.isnan(ref["M_total"][-1, :5]).all() and np.isfinite(ref["M_total"][-1, 5:]).all()
+    assert abs(m.n[1] * 86400.0 - (nsteps - 72)) < 1e-6  # cell 1's n froze while its NaN slot was in the window
+    if engine == "float64":
+        ok_steps = np.ones((nsteps, 8), dtype=bool)
+    else:
+        flip, genuine = melt_out_flips(outs, ref, 1e-5)
+        assert not genuine, genuine
+        assert (flip >= 0).sum() <= 1, flip
+        ok_steps = valid_mask(flip, nsteps)
     for v in HIST:
         np.testing.assert_array_equal(np.isnan(outs[v]), np.isnan(ref[v]), err_msg=v)
-        ok = ~np.isnan(ref[v])
-        assert _rel(outs[v][ok], ref[v][ok]) <= 1e-10, v
-    assert np.isnan(ref["M_total"][-1, :5]).all() and np.isfinite(ref["M_total"][-1, 5:]).all()
+        ok = ~np.isnan(ref[v]) & ok_steps
+        if engine == "float64":
+            assert _rel(outs[v][ok], ref[v][ok]) <= 1e-10, v
+        else:
+            assert parity(outs[v], np.where(np.isnan(ref[v]), 0.0, ref[v]), mask=ok)[0] <= 1e-5, v
+    keep = ok_steps[-1]
+    for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n"):
+        want = np.asarray(getattr(m, v), np.float64)
+        np.testing.assert_array_equal(np.isnan(state[v]), np.isnan(want), err_msg=v)
+        fin = np.isfinite(want) & keep
+        tol = 1e-10 if engine == "float64" else 1e-5
+        assert parity(state[v], want, mask=fin)[0] <= tol, (v, state[v], want)
+    assert state["n"][1] == m.n[1]  # frozen over the 72 steps the NaN slot spent in the window
     np.testing.assert_array_equal(np.isnan(diag[0, :5]), np.isnan([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM]))
 
 

@@ -289,6 +289,22 @@ def test_library_is_built_from_these_sources():
     assert f"tfg-src-sha256={G.built_hash(G.LIB)}" in info
     assert G.built_hash(G.LIB) == G.source_hash(G.build_flags()), "stale _tfg.so: run __graft_entry__.build()"
     assert _native.code_object_sha256() is not None
+    assert _native.kernel_code_sha256() is not None
+
+
+def test_pmc_provenance_follows_the_timed_kernel_only(tmp_path):
+    """bench.py quotes PMC traffic by the timed kernel's own machine code
+    (_native.kernel_code_sha256).  A build that changes only another kernel
+    (the ice-flow prefetch variant) changes the library's device code but not
+    that hash; a build that changes k_fused's stores changes it."""
+    import __graft_entry__ as G
+    from topoflow_glacier import _native
+
+    other = G.build_engine(["-DTFG_FLOW_PF2"], out=tmp_path / "flow.so", verbose=False)
+    mine = G.build_engine(["-DTFG_NT_STORE=0"], out=tmp_path / "nt.so", verbose=False)
+    assert _native.code_object_sha256(other) != _native.code_object_sha256()
+    assert _native.kernel_code_sha256(path=other) == _native.kernel_code_sha256()
+    assert _native.kernel_code_sha256(path=mine) != _native.kernel_code_sha256()
 
 
 def test_bmi_one_cell_path_does_not_need_torch():

@@ -522,12 +522,12 @@ __global__ void k_window_set(int32_t* __restrict__ slot, const double* __restric
 }
 __global__ void k_window_get(double* __restrict__ v, const int32_t* __restrict__ slot, int64_t n, double inv_qscale) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    v[i] = (double)slot[i] * inv_qscale;
+    v[i] = slot[i] == tfg::kWindowNan ? (double)NAN : (double)slot[i] * inv_qscale;
 }
 __global__ void k_window_total(int64_t* __restrict__ tot, const int32_t* __restrict__ ring, int ring_len, int64_t n_pad) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t t = 0;
-    for (int s = 0; s < ring_len; ++s) t += ring[(int64_t)s * n_pad + i];
+    for (int s = 0; s < ring_len; ++s) t += tfg::window_tot(ring[(int64_t)s * n_pad + i]);
     tot[i] = t;
   }
 }

@@ -115,12 +115,30 @@ __device__ __forceinline__ double pyremainder(double a, double b) {
 // step (:1027-1041); only the predicate sum >= 0.03 is used.  A fixed-point
 // running total decides it exactly up to ring_len*2^-37 (< 2.2e-9 at 288
 // slots), with no drift.
+//
+// Missing data: a NaN snowfall (NaN forcing P) makes the reference's window
+// sum NaN for as long as the slot stays in the ring, and then neither
+// np.where of :1040-1041 fires, so n freezes.  A NaN slot is stored as the
+// sentinel kWindowNan (no finite value quantises to it) and counts
+// kWindowNanTot in the running total: |sum of finite slots| < 288 * 2^31 <
+// 2^40, so the total is >= 2^43 exactly while a NaN slot is in the window.
+constexpr int32_t kWindowNan = (int32_t)0x80000000;
+constexpr int64_t kWindowNanTot = (int64_t)1 << 44;
+constexpr int64_t kWindowNanMin = (int64_t)1 << 43;
 __device__ __forceinline__ int32_t window_q(double v, double qscale) {
   double s = v * qscale;
-  if (!(s == s)) return 0;
+  if (!(s == s)) return kWindowNan;
   if (s > 2147483647.0) return 2147483647;
   if (s < -2147483647.0) return -2147483647;
   return (int32_t)__double2ll_rn(s);
+}
+// A slot's contribution to the running total.
+__device__ __forceinline__ int64_t window_tot(int32_t q) { return q == kWindowNan ? kWindowNanTot : (int64_t)q; }
+// Days since the last major snowfall (:1040-1041): reset where the window
+// total reaches 0.03 m, advanced where it stays below, unchanged while the
+// total is NaN (a NaN slot in the window).
+__device__ __forceinline__ double window_days(double n, int64_t tot_q, int64_t thr_q, double days_per_dt) {
+  return tot_q >= kWindowNanMin ? n : (tot_q >= thr_q ? 0.0 : n + days_per_dt);
 }
 
 // ---------------------------------------------------------------------------
@@ -246,10 +264,10 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
 }
 
 // Albedo ageing (:1020-1059) given the window predicate (exact variant).
-__device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st, bool wet_window, double T_air) {
+__device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st, double T_air) {
 #pragma clang fp contract(off)  // 0.4 + 0.44 * exp(...) rounds the product first, as numpy does
   // n: where(tot >= .03, 0, n); where(tot < .03, n + days_per_dt, n)
-  st.n = wet_window ? 0.0 : st.n + p.days_per_dt;
+  st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
   const double r = (T_air > 0.0) ? 0.12 : 0.05;
   const double snow_albedo = 0.4 + 0.44 * exp(-st.n * r);
   double albedo = (st.h_snow > 0.0) ? snow_albedo : st.albedo;
@@ -374,8 +392,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
   // albedo :1023-1059 with the fixed-point window
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
-  st.tot_q += (int64_t)q_new - (int64_t)q_old;
-  const double albedo = albedo_step(p, st, st.tot_q >= p.thr_q, T_air);
+  st.tot_q += window_tot(q_new) - window_tot(q_old);
+  const double albedo = albedo_step(p, st, T_air);
   const DevParams& p2 = params();  // Clear_Sky_Radiation phase
   // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
   const double a_sa = -0.1240 - (0.0207 * W_p);
@@ -493,8 +511,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double T_air_K = T_air + 273.15;
   // window and days since snowfall (:1023-1040), ahead of the albedo exp
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
-  st.tot_q += (int64_t)q_new - (int64_t)q_old;
-  st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
+  st.tot_q += window_tot(q_new) - window_tot(q_old);
+  st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
   const double r_alb = (T_air > 0.0) ? 0.12 : 0.05;
 
   // ---- level 1: arguments from inputs, state, statics and uniforms
@@ -788,10 +806,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const bool snow_pos = st.h_snow > 0.0, ice_pos = st.h_ice > 0.0;  // previous-step depths
   const float T_K = T_air + 273.15f;
   const float rT = frcp(T_K);
-  // rain/snow split (:578-604): T_air > T_rs, exact via the rounded-down threshold
-  const bool is_rain = T_air > p.f_T_rs_dn;
-  const float P_rain = is_rain ? P : P * 0.0f;
-  const float P_snow = is_rain ? P * 0.0f : P;
+  // rain/snow split (:578-604): T_air > T_rs, exact via the rounded-down
+  // threshold; both tests written out, so a NaN T_air gives P * 0 for both,
+  // as the reference's P * (T > T_rs) and P * (T <= T_rs) do
+  const float P_rain = (T_air > p.f_T_rs_dn) ? P : P * 0.0f;
+  const float P_snow = (T_air <= p.f_T_rs_dn) ? P : P * 0.0f;
   d.P += P;
   d.Pmax = npmax(d.Pmax, P);
   d.PR += P_rain;
@@ -822,13 +841,13 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float log_term = flog2(e_air) * kLn2 - 1.8102704f;
 #endif
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
-  const float T_surf = (snow_pos || ice_pos) ? fminf(T_dew, 0.0f) : T_dew;
+  const float T_surf = (snow_pos || ice_pos) ? npmin(T_dew, 0.0f) : T_dew;
   // turbulent fluxes (:640-745, :919-934)
   const float dTs = T_air - T_surf;
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
   const float Ri = p.f_gz * dTs * frcp(bot);
-  const float L2 = flog2_split(fmaxf((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
+  const float L2 = flog2_split(npmax((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
   const float Dn = uz * p.f_k2 * frcp(L2 * L2);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
   // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
@@ -853,10 +872,10 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // snowfall window + albedo ageing (:1006-1059)
   {
     const float sq = P_snow * p.f_qfac;  // P_snow*dt*ws*2^36
-    q_new = (sq == sq) ? (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f)) : 0;
+    q_new = (sq == sq) ? (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f)) : kWindowNan;
   }
-  st.tot_q += (int64_t)q_new - (int64_t)q_old;
-  st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
+  st.tot_q += window_tot(q_new) - window_tot(q_old);
+  st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
   float albedo;
   {
     // selects in fp32: albedo is rebuilt every step from n and the depths
@@ -871,11 +890,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   }
   // clear-sky shortwave (SF:904-941); W_p = 1.12*w
   const float w = fexp2((0.0614f * kLog2e) * T_dew);
-  const float tau = fminf(fmaxf(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);
+  const float tau = npmin(npmax(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);  // SF:614
   const float gam_s = p.f_1pdust - fexp2(fmaf(u.gam_c1, w, u.gam_c0));
   // cos(lat_eq)*cos(omega*th + dlon)
   const float cwl = u.cos_wth_f * g.cc - u.sin_wth_f * g.cs;
-  const float K_ET = fmaxf(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);
+  const float K_ET = npmax(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);  // SF:887
   const float kf = u.k_et_flat_f;
   const float K_dif = 0.5f * gam_s * kf;
   const float K_bs = 0.5f * gam_s * albedo * fmaf(tau, kf, K_dif);
@@ -910,41 +929,43 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
   if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
 
-  // ---- state update (:1566-1731), fp64 where depths and cold contents accumulate
+  // ---- state update (:1566-1731), fp64 where depths and cold contents accumulate.
+  // max / min as numpy's np.maximum / np.minimum (NaN-propagating), so missing
+  // forcing turns the same outputs NaN as in the reference
   const double previous_swe = st.h_swe;
   const double E_in = (double)(Q_sum * p.f_dt);
   // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
-  const double E_rem_s = fmax(E_in - st.Eccs, 0.0);
+  const double E_rem_s = npmax(E_in - st.Eccs, 0.0);
   d.Erem_s += (float)E_rem_s;
   // update_swe (:1594-1606)
   double h_swe = add_rounded(st.h_swe, (double)P_snow, p.dt);
-  const double ts = fmin(E_rem_s * p.c_sm3600, h_swe);
+  const double ts = npmin(E_rem_s * p.c_sm3600, h_swe);
   const double SM = ts * (1.0 / 3600.0);
-  h_swe = fmax(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
+  h_swe = npmax(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
   // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
   double Eccs = st.Eccs;
-  const bool snowing = P_snow > 0.0f;
-  if (snowing) {
+  if (P_snow > 0.0f) {
     const float rh = RH;
     const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
                        fast_atanf(rh - 1.676331f) +
                        (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
-    Eccs = fmax(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
+    Eccs = npmax(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
   }
   // ice melt (:1418-1434), cap (:1473-1480), integral (:1493), update_iwe (:1612-1617)
-  const double E_rem_i = fmax(E_in - st.Ecci, 0.0);
+  const double E_rem_i = npmax(E_in - st.Ecci, 0.0);
   double IM = (h_swe == 0.0 && previous_swe == 0.0) ? E_rem_i * p.inv_dt_rhoLf : 0.0;
-  double Ecci = fmax(st.Ecci - E_in, 0.0);
+  double Ecci = npmax(st.Ecci - E_in, 0.0);
   Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;
-  IM = fmin(IM, st.h_iwe * p.inv_dt);
+  IM = npmin(IM, st.h_iwe * p.inv_dt);  // max(IM, 0) is implied (IM, h_iwe >= 0 or NaN)
   d.IM += (float)IM;
-  const double ti = fmin(IM * 3600.0, st.h_iwe);
+  const double ti = npmin(IM * 3600.0, st.h_iwe);
   IM = ti * (1.0 / 3600.0);
-  const double h_iwe = fmax(sub_rounded(st.h_iwe, IM, p.dt3600), 0.0);
-  // depths (:1711, :1726), snowpack cold content (:1556-1558, new h_snow)
+  const double h_iwe = npmax(sub_rounded(st.h_iwe, IM, p.dt3600), 0.0);
+  // depths (:1711, :1726), snowpack cold content (:1556-1558, new h_snow);
+  // P_snow <= 0 written out: a NaN snowfall leaves Eccs alone, as np.where does
   const double h_snow = h_swe * p.ws;
   const double h_ice = h_iwe * p.wi;
-  if (!snowing) Eccs = fmax(Eccs - E_in, 0.0);
+  if (P_snow <= 0.0f) Eccs = npmax(Eccs - E_in, 0.0);
   Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
   st.h_swe = h_swe;
   st.h_iwe = h_iwe;

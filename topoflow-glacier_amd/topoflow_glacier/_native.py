@@ -162,6 +162,109 @@ def code_object_sha256(path: Path | None = None) -> str | None:
     return hashlib.sha256(blob).hexdigest() if blob else None
 
 
+BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1E"  # k_fused<float, false, false, false, false, 1>
+
+
+def gfx950_code_objects(path: Path | None = None) -> list[bytes]:
+    """The gfx950 code objects (ELF) in the library's ``.hip_fatbin`` section:
+    one clang offload bundle per translation unit, each holding a host entry
+    and the device image (magic, entry count, then offset/size/triple per entry,
+    offsets from the bundle's start)."""
+    import struct
+
+    blob = elf_section(Path(path or LIB_PATH), ".hip_fatbin") or b""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out, pos = [], blob.find(magic)
+    while pos >= 0:
+        n_entries, = struct.unpack_from("<Q", blob, pos + len(magic))
+        o = pos + len(magic) + 8
+        for _ in range(n_entries):
+            off, size, tlen = struct.unpack_from("<QQQ", blob, o)
+            triple = blob[o + 24:o + 24 + tlen].decode()
+            o += 24 + tlen
+            if triple.endswith("gfx950") and size:
+                out.append(blob[pos + off:pos + off + size])
+        pos = blob.find(magic, pos + 1)
+    return out
+
+
+def _elf_symbols(elf: bytes):
+    """(name, value, size, type, section bytes, section address) of every sized
+    symbol of a 64-bit ELF."""
+    import struct
+
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, _ = struct.unpack_from("<HHH", elf, 0x3A)
+    sec = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+    syms = []
+    for _name, typ, _fl, _addr, off, size, link, _info, _al, entsize in sec:
+        if typ != 2:  # SHT_SYMTAB
+            continue
+        stroff = sec[link][4]
+        for j in range(size // entsize):
+            st_name, st_info, _other, st_shndx, st_value, st_size = struct.unpack_from("<IBBHQQ", elf, off + j * entsize)
+            if st_size == 0 or st_shndx == 0 or st_shndx >= shnum:
+                continue
+            end = elf.index(b"\0", stroff + st_name)
+            s = sec[st_shndx]
+            syms.append((elf[stroff + st_name:end].decode(), st_value, st_size, st_info & 0xF, s[3], s[4]))
+    return syms
+
+
+def kernel_code_sha256(symbol_prefix: str = BENCH_KERNEL, path: Path | None = None) -> str | None:
+    """sha256 of ONE kernel's gfx950 machine code: its instructions, its kernel
+    descriptor (register counts, LDS, launch attributes) and, transitively, the
+    code and data it reaches through PC-relative addressing (e.g. the
+    __noinline__ dark_exact).  The PC-relative literals themselves are masked
+    (s_getpc_b64 followed by s_add_u32 / s_addc_u32 with a literal) and so is
+    the descriptor's entry offset: moving other kernels around in the code
+    object, or changing them, leaves the hash alone, while any change to the
+    instructions this kernel executes changes it.  bench.py quotes a PMC
+    traffic profile only for the kernel code it was measured on."""
+    import hashlib
+    import struct
+
+    for elf in gfx950_code_objects(path):
+        syms = _elf_symbols(elf)
+        entry = [s for s in syms if s[0].startswith(symbol_prefix) and s[3] == 2]  # STT_FUNC
+        if not entry:
+            continue
+        by_addr = {s[1]: s for s in syms}
+        h = hashlib.sha256()
+        seen, todo = set(), [entry[0]]
+        while todo:
+            name, value, size, typ, sec_addr, sec_off = todo.pop(0)
+            if value in seen:
+                continue
+            seen.add(value)
+            code = bytearray(elf[sec_off + value - sec_addr:sec_off + value - sec_addr + size])
+            if typ == 2:
+                words = len(code) // 4
+                for w in range(words - 4):
+                    (ins,) = struct.unpack_from("<I", code, 4 * w)
+                    if (ins & 0xFF80FF00) != 0xBE801C00:  # s_getpc_b64 sN (SOP1, opcode 28)
+                        continue
+                    pc = value + 4 * w + 4
+                    (add,) = struct.unpack_from("<I", code, 4 * w + 4)
+                    (addc,) = struct.unpack_from("<I", code, 4 * w + 12)
+                    if (add >> 23) == 0x100 and (addc >> 23) == 0x104 and 0xFF in (add & 0xFF, (add >> 8) & 0xFF):
+                        lo, = struct.unpack_from("<i", code, 4 * w + 8)
+                        for t in (pc + lo, pc + lo - 4):  # @rel32@lo+4: the literal is target - pc + 4
+                            if t in by_addr:
+                                todo.append(by_addr[t])
+                        struct.pack_into("<I", code, 4 * w + 8, 0)
+                        struct.pack_into("<I", code, 4 * w + 16, 0)
+            h.update(name.encode() + b"\0" + bytes(code))
+        kd = [s for s in syms if s[0] == entry[0][0] + ".kd"]
+        if kd:
+            name, value, size, _t, sec_addr, sec_off = kd[0]
+            d = bytearray(elf[sec_off + value - sec_addr:sec_off + value - sec_addr + size])
+            d[16:24] = bytes(8)  # kernel_code_entry_byte_offset: where the code object put the kernel
+            h.update(b"kd\0" + bytes(d))
+        return h.hexdigest()
+    return None
+
+
 def lib() -> ctypes.CDLL:
     return load()
 
