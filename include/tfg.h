@@ -267,6 +267,19 @@ int tfg_reset_diag(tfg_handle* h);
 /* Wait for all work queued on the handle's stream. */
 int tfg_sync(tfg_handle* h);
 
+/* Missing data (fp32 engine).  The reference's numpy arithmetic propagates NaN
+ * (np.maximum / np.minimum, the NaN window sum freezing n; :1035-1041,
+ * :1364-1434).  Each launch of the fp32 engine runs its clean step form when
+ * everything the launch reads (its forcing frames or tfg_update's inputs, the
+ * elevation raster, the Qc plane in use, the state and the snowfall window) is
+ * known to be finite, and its NaN-safe form otherwise; the results agree
+ * wherever the data is finite.  Finiteness is checked where data enters
+ * (tfg_set_field, tfg_set_inputs and tfg_update from host memory) and, for
+ * launches of 8 or more steps, lazily before the launch (a synchronous device
+ * check) where it is unknown.  *count = launches that ran the NaN-safe form.
+ * The environment variable TFG_NANSAFE=1 at tfg_create forces that form. */
+int tfg_nan_safe_launches(tfg_handle* h, int64_t* count);
+
 /* Device-side synthetic workload generator (bench / tests): fills the forcing
  * frames, static rasters and initial depths from a counter-based hash of
  * (seed, field, frame, global cell index).  `row0` is this shard's first row in

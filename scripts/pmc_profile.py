@@ -80,7 +80,7 @@ def main():
     wr = raw["WRITE_SIZE"] * 1024 * wr_scale
     alg = nx * ny * launch_bytes_per_cell(fuse)
     res = {
-        "kernel": f"k_fused<float,false,false,false,1> (fp32 engine, {fuse} steps fused) at {nx}x{ny}",
+        "kernel": f"k_fused<float,false,false,false,false,1,false> (fp32 engine, clean form, {fuse} steps fused) at {nx}x{ny}",
         "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "
                    "calibration: rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE -- tools/hbm_mix 67108864 8 2048 0 cal); "
                    "python3 scripts/pmc_profile.py",

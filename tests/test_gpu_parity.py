@@ -785,3 +785,72 @@ def test_checkpoint_restart_is_bit_exact(tmp_path, engine):
         e.close()
     for k in runs[0]:
         np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
+
+
+def test_fp32_step_forms_agree_on_finite_data_and_the_engine_picks_them(monkeypatch):
+    """The fp32 engine's two step forms (tfg_physics.hpp, "Missing data"): on
+    finite data the NaN-safe form equals the clean form bit for bit (outputs,
+    state, window slots, diagnostics).  A finite run takes the clean form in
+    every launch; a NaN in one forcing frame sends the launches that read it,
+    and (through the state it leaves) the launches after, to the NaN-safe form;
+    TFG_NANSAFE=1 forces it everywhere."""
+    g = load_golden("grid64")
+    nsteps = 100
+    runs = {}
+    for mode in ("clean", "forced"):
+        if mode == "forced":
+            monkeypatch.setenv("TFG_NANSAFE", "1")
+        else:
+            monkeypatch.delenv("TFG_NANSAFE", raising=False)
+        e = make_engine(g["cfg"], 8, 8, "float32", n_frames=nsteps, hist_depth=nsteps, fuse_steps=24)
+        try:
+            for k in ("elev", "slope", "aspect"):
+                e.set_field(k, g["static"][k])
+            for k in ("h_snow", "h_ice", "h_swe", "h_iwe"):
+                e.set_field(k, g["static"]["h0_" + k[2:]])
+            e.init_state()
+            for k in range(nsteps):
+                for name in ("P", "T_air", "Hum_sp", "P_air", "uz"):
+                    e.set_field(name, np.asarray(g["forcing"][name][k]), index=k)
+            e.run(nsteps, frames=np.arange(nsteps, dtype=np.int32))
+            e.sync()
+            runs[mode] = ({v: np.stack([e.get_field(v, index=k) for k in range(nsteps)]) for v in HIST},
+                          {v: e.get_field(v) for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")},
+                          np.stack([e.get_field("window", index=j) for j in range(e.ring_len)]), e.diagnostics(),
+                          e.nan_safe_launches())
+        finally:
+            e.close()
+    (oa, sa, wa, da, na), (ob, sb, wb, db, nb) = runs["clean"], runs["forced"]
+    assert na == 0 and nb == 5  # 100 steps in launches of 24
+    for v in HIST:
+        np.testing.assert_array_equal(oa[v], ob[v], err_msg=v)
+    for v in sa:
+        np.testing.assert_array_equal(sa[v], sb[v], err_msg=v)
+    np.testing.assert_array_equal(wa, wb)
+    np.testing.assert_array_equal(da, db)
+    # a NaN in frame 30: launches 0 (steps 0-23) clean, 1 (24-47) NaN-safe; then
+    # the state is checked before each launch and holds the NaN for good
+    monkeypatch.delenv("TFG_NANSAFE", raising=False)
+    e = make_engine(g["cfg"], 8, 8, "float32", n_frames=nsteps, hist_depth=nsteps, fuse_steps=24)
+    try:
+        for k in ("elev", "slope", "aspect"):
+            e.set_field(k, g["static"][k])
+        for k in ("h_snow", "h_ice", "h_swe", "h_iwe"):
+            e.set_field(k, g["static"]["h0_" + k[2:]])
+        e.init_state()
+        for k in range(nsteps):
+            for name in ("P", "T_air", "Hum_sp", "P_air", "uz"):
+                x = np.array(g["forcing"][name][k], copy=True)
+                if k == 30 and name == "P_air":
+                    x[5] = np.nan
+                e.set_field(name, x, index=k)
+        e.run(24, frames=np.arange(24, dtype=np.int32))
+        assert e.nan_safe_launches() == 0
+        e.run(24, frames=np.arange(24, 48, dtype=np.int32))
+        assert e.nan_safe_launches() == 1
+        e.run(52, frames=np.arange(48, 100, dtype=np.int32))
+        e.sync()
+        assert e.nan_safe_launches() == 4
+        assert np.isnan(e.get_field("Eccs")[5]) and np.isfinite(np.delete(e.get_field("Eccs"), 5)).all()
+    finally:
+        e.close()

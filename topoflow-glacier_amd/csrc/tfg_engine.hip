@@ -532,6 +532,25 @@ __global__ void k_window_total(int64_t* __restrict__ tot, const int32_t* __restr
   }
 }
 
+// Non-finite checks behind the fp32 engine's choice of step form (see
+// tfg_handle::plane_state): flag |= 1 where a value is NaN or infinite, or
+// where a window total holds a NaN slot.
+template <class T>
+__global__ void k_nonfinite(const T* __restrict__ p, int64_t n, int32_t* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(p[i]);
+  if (bad) atomicOr(flag, 1);
+}
+__global__ void k_window_nan(const int64_t* __restrict__ tot, int64_t n, int32_t* __restrict__ flag) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= tot[i] >= tfg::kWindowNanMin;
+  if (bad) atomicOr(flag, 1);
+}
+
+enum : uint8_t { kUnknown = 0, kOk = 1, kDirty = 2 };
+
 struct tfg_handle {
   int device = 0, engine = TFG_F32;
   int64_t ny = 0, nx = 0, n = 0, n_pad = 0;
@@ -596,6 +615,17 @@ struct tfg_handle {
   size_t io_cap = 0;
   uint32_t io_seq = 0;
   int64_t last_hist = 0;
+  // Finite-data tracking for the fp32 engine's two step forms (tfg_physics.hpp,
+  // "Missing data"): a launch runs the clean form only when everything it reads
+  // is known to be finite.  kUnknown: written by a path that did not check it;
+  // kDirty: checked, holds a NaN or an infinity.
+  std::vector<uint8_t> plane_state;  // [n_frames][kNumForc] forcing planes
+  uint8_t state_state = 1;           // fp64 state planes and the snowfall window
+  uint8_t elev_state = 1;            // the elevation raster (the fp32 flux reads it unguarded)
+  uint8_t qc_state = 1;              // the Qc plane while the conduction term is on
+  int state_recheck = 0;             // launches before a dirty state is checked again
+  int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
+  bool force_ns = false;             // TFG_NANSAFE=1: every launch NaN-safe (tests)
   std::string err;
 };
 
@@ -660,6 +690,30 @@ int upload(tfg_handle* h, void* dst, int dt, const void* src, int st, int64_t n,
   HIPCHK(h, hipGetLastError());
   if (!on_dev) HIPCHK(h, hipStreamSynchronize(h->stream));
   return TFG_OK;
+}
+
+// kOk when every one of `count` values at device pointer p is finite, kDirty
+// otherwise (synchronous).
+int check_finite(tfg_handle* h, const void* p, int dtype, int64_t count, uint8_t* out) {
+  HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
+  if (dtype == TFG_F64)
+    hipLaunchKernelGGL((k_nonfinite<double>), grid_for(count), 256, 0, h->stream, (const double*)p, count, h->d_flag);
+  else
+    hipLaunchKernelGGL((k_nonfinite<float>), grid_for(count), 256, 0, h->stream, (const float*)p, count, h->d_flag);
+  HIPCHK(h, hipGetLastError());
+  int32_t flag = 0;
+  HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  *out = flag ? kDirty : kOk;
+  return TFG_OK;
+}
+
+// The same check on host values (the BMI inputs of tfg_update / tfg_set_inputs).
+template <class T>
+uint8_t host_finite(const T* p, int64_t n) {
+  bool bad = false;
+  for (int64_t i = 0; i < n; ++i) bad |= !std::isfinite(p[i]);
+  return bad ? kDirty : kOk;
 }
 
 int download(tfg_handle* h, void* dst, int dt, const void* src, int st, int64_t n, int on_dev) {
@@ -809,10 +863,11 @@ struct IoArgs {
   double* out = nullptr;
   uint32_t* flag = nullptr;
   uint32_t seq = 0;
+  uint8_t in_state = kUnknown;  // the inputs' finite-data status (tfg_handle::plane_state)
 };
 
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io = IoArgs()) {
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns) {
   KArgs a;
   a.p = h->dp;
   a.K = K;
@@ -834,18 +889,22 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   constexpr int C = kCellsPerThread;
 #define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, \
                  h->slab, (const R*)h->qc
-#define TFG_LAUNCH(RD, CT, QC) hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C>), blocks, kBlock, lds, h->stream, TFG_ARGS)
+#define TFG_LAUNCH(RD, CT, QC, NS) \
+  hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C, NS>), blocks, kBlock, lds, h->stream, TFG_ARGS)
+#define TFG_LAUNCH_NS(RD, CT, QC) \
+  do { if (ns) TFG_LAUNCH(RD, CT, QC, true); else TFG_LAUNCH(RD, CT, QC, false); } while (0)
   if (h->qc_on) {  // the optional lateral conduction term (tfg_conduction_update / TFG_ST_QC)
-    if (rd && ct) TFG_LAUNCH(true, true, true);
-    else if (rd) TFG_LAUNCH(true, false, true);
-    else if (ct) TFG_LAUNCH(false, true, true);
-    else TFG_LAUNCH(false, false, true);
+    if (rd && ct) TFG_LAUNCH_NS(true, true, true);
+    else if (rd) TFG_LAUNCH_NS(true, false, true);
+    else if (ct) TFG_LAUNCH_NS(false, true, true);
+    else TFG_LAUNCH_NS(false, false, true);
   } else {
-    if (rd && ct) TFG_LAUNCH(true, true, false);
-    else if (rd) TFG_LAUNCH(true, false, false);
-    else if (ct) TFG_LAUNCH(false, true, false);
-    else TFG_LAUNCH(false, false, false);
+    if (rd && ct) TFG_LAUNCH_NS(true, true, false);
+    else if (rd) TFG_LAUNCH_NS(true, false, false);
+    else if (ct) TFG_LAUNCH_NS(false, true, false);
+    else TFG_LAUNCH_NS(false, false, false);
   }
+#undef TFG_LAUNCH_NS
 #undef TFG_LAUNCH
 #undef TFG_ARGS
   HIPCHK(h, hipGetLastError());
@@ -949,6 +1008,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // handle keeps one row, not 32768 (NextGen may hold thousands of handles)
   h->max_blocks = (int)std::min<int64_t>(h->max_blocks, (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);
   if (const char* e = std::getenv("TFG_FUSE")) h->fuse = std::max(1, atoi(e));
+  if (const char* e = std::getenv("TFG_NANSAFE")) h->force_ns = atoi(e) != 0;
   if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "stream create failed"; return bail(TFG_ERR_HIP); }
   h->stream = h->own_stream;
   const int64_t np = h->n_pad;
@@ -975,6 +1035,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
     if (hipMemsetAsync(*a.p, 0, a.bytes, h->stream) != hipSuccess) { h->err = "hipMemset failed"; return bail(TFG_ERR_HIP); }
   }
   if (hipStreamSynchronize(h->stream) != hipSuccess) { h->err = "sync failed"; return bail(TFG_ERR_HIP); }
+  h->plane_state.assign((size_t)n_frames * kNumForc, kOk);  // zero-filled: finite
   *out = h;
   return TFG_OK;
 }
@@ -1077,10 +1138,12 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     return TFG_OK;
   }
   if (src_dtype != TFG_F32 && src_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "src dtype must be TFG_F32/TFG_F64");
+  const bool track = h->engine == TFG_F32;  // finite-data tracking (tfg_handle::plane_state)
   if (field == TFG_ST_QC) {  // a caller-supplied conduction flux: on until tfg_conduction_off
     if (int rc = ensure_qc(h)) return rc;
     if (int rc = upload(h, h->qc, h->engine, src, src_dtype, n, src_on_device)) return rc;
     h->qc_on = true;
+    if (track) return check_finite(h, h->qc, h->engine, n, &h->qc_state);
     return TFG_OK;
   }
   if (field == TFG_ST_WINDOW) {
@@ -1092,6 +1155,11 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
                        h->dp.qscale);
     HIPCHK(h, hipGetLastError());
     h->tot_dirty = true;
+    if (track) {  // a NaN slot makes the window dirty; a finite one leaves the state's status as it was
+      uint8_t st = kOk;
+      if (int rc = check_finite(h, h->wtmp, TFG_F64, n, &st)) return rc;
+      if (st != kOk) h->state_state = kDirty;
+    }
     return TFG_OK;
   }
   int fdt = 0;
@@ -1109,10 +1177,27 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     double* sd = h->st + (field == TFG_OUT_H_SNOW ? S_HSNOW : S_HICE) * h->n_pad;
     int rc = upload(h, sd, TFG_F64, src, src_dtype, n, src_on_device);
     if (rc) return rc;
+    if (track) {
+      uint8_t st = kOk;
+      if (int rc2 = check_finite(h, sd, TFG_F64, n, &st)) return rc2;
+      if (st != kOk) h->state_state = kDirty;
+    }
     return upload(h, dst, fdt, src, src_dtype, n, src_on_device);
   }
   int rc = upload(h, dst, fdt, src, src_dtype, n, src_on_device);
   if (rc) return rc;
+  if (track && is_frame_field(field)) {
+    const int plane = field == TFG_IN_P ? F_P : field == TFG_IN_T_AIR ? F_T : field == TFG_IN_HUM_SP ? F_Q
+                    : field == TFG_IN_P_AIR ? F_PA : F_UZ;
+    if (int rc2 = check_finite(h, dst, fdt, n, &h->plane_state[(size_t)index * kNumForc + plane])) return rc2;
+  } else if (track && field == TFG_ST_ELEV) {
+    if (int rc2 = check_finite(h, dst, fdt, n, &h->elev_state)) return rc2;
+  } else if (track && (field == TFG_OUT_H_SWE || field == TFG_OUT_H_IWE || field == TFG_ST_ECCS || field == TFG_ST_ECCI ||
+                       field == TFG_ST_ALBEDO || field == TFG_ST_NDAYS)) {
+    uint8_t st = kOk;
+    if (int rc2 = check_finite(h, dst, fdt, n, &st)) return rc2;
+    if (st != kOk) h->state_state = kDirty;
+  }
   if (field == TFG_ST_ELEV || field == TFG_ST_SLOPE || field == TFG_ST_ASPECT) h->geo_dirty = true;
   if (field == TFG_ST_SLOPE) {
     HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
@@ -1238,6 +1323,62 @@ int prepare_steps(tfg_handle* h) {
   return TFG_OK;
 }
 
+// Launches of at least this many steps check unknown data before choosing the
+// fp32 step form (a synchronous device check); shorter ones run NaN-safe.
+constexpr int kVerifySteps = 8;
+
+// The state's finite-data status: the fp64 state planes and the window totals
+// (after prepare_steps has rebuilt them).  Synchronous.
+int check_state(tfg_handle* h) {
+  uint8_t st = kOk;
+  if (int rc = check_finite(h, h->st, TFG_F64, (int64_t)kNumState * h->n_pad, &st)) return rc;
+  if (st == kOk) {
+    HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
+    hipLaunchKernelGGL(k_window_nan, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->n_pad, h->d_flag);
+    HIPCHK(h, hipGetLastError());
+    int32_t flag = 0;
+    HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    st = flag ? kDirty : kOk;
+  }
+  h->state_state = st;
+  return TFG_OK;
+}
+
+// The fp32 engine's step form for one launch of K steps (tfg_physics.hpp,
+// "Missing data"): the clean form when the launch's forcing frames (or the
+// tfg_update inputs), the elevation raster, the Qc plane in use, the state and
+// the window are known to hold only finite values; the NaN-safe form
+// otherwise.  Unknown data is checked first when the launch is long enough to
+// pay for a synchronous check.
+int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, bool* ns) {
+  const bool check = K >= kVerifySteps;
+  bool inputs_ok = true;
+  if (io.in) {
+    inputs_ok = io.in_state == kOk;
+  } else {
+    for (int k = 0; k < K; ++k) {
+      uint8_t* ps = &h->plane_state[(size_t)u[k].frame * kNumForc];
+      for (int f = 0; f < kNumForc; ++f) {
+        if (ps[f] == kUnknown && check) {
+          char* plane = static_cast<char*>(h->forc) + ((size_t)u[k].frame * kNumForc + f) * h->n_pad * h->rsz;
+          if (int rc = check_finite(h, plane, h->engine, h->n, &ps[f])) return rc;
+        }
+        inputs_ok &= ps[f] == kOk;
+      }
+    }
+  }
+  if (check && (h->state_state == kUnknown || (h->state_state == kDirty && --h->state_recheck <= 0))) {
+    if (int rc = check_state(h)) return rc;
+    if (h->state_state == kDirty) h->state_recheck = kVerifySteps;  // launches until the next look
+  }
+  if (h->qc_on && h->qc_state == kUnknown && check)
+    if (int rc = check_finite(h, h->qc, h->engine, h->n, &h->qc_state)) return rc;
+  *ns = h->force_ns ||
+        !(inputs_ok && h->state_state == kOk && h->elev_state == kOk && (!h->qc_on || h->qc_state == kOk));
+  return TFG_OK;
+}
+
 int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
                  const IoArgs& io = IoArgs()) {
   if (int rc = prepare_steps(h)) return rc;
@@ -1264,9 +1405,17 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
                          static_cast<double*>(h->hist), h->slab, h->qc_on ? static_cast<const double*>(h->qc) : nullptr,
                          h->depths_derived ? 0 : 1);
       HIPCHK(h, hipGetLastError());
+    } else if (h->engine == TFG_F32) {
+      bool ns = true;
+      if ((rc = choose_form(h, u + k0, K, io, &ns))) return rc;
+      rc = launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, ns);
+      if (ns) {
+        ++h->ns_launches;
+        // the NaN-safe form may have carried missing data into the state
+        if (h->state_state == kOk) h->state_state = kUnknown;
+      }
     } else {
-      rc = (h->engine == TFG_F32) ? launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io)
-                                  : launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io);
+      rc = launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, false);
     }
     if (rc) return rc;
     h->depths_derived = true;
@@ -1328,6 +1477,12 @@ int tfg_reset_diag(tfg_handle* h) {
   return TFG_OK;
 }
 
+int tfg_nan_safe_launches(tfg_handle* h, int64_t* count) {
+  if (!h || !count) return fail(h, TFG_ERR_ARG, "null argument");
+  *count = h->ns_launches;
+  return TFG_OK;
+}
+
 int tfg_sync(tfg_handle* h) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
@@ -1354,6 +1509,10 @@ int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_gl
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->slope_invalid = false;
   h->geo_dirty = true;
+  // the generator writes finite forcing, statics and depths
+  std::fill(h->plane_state.begin(), h->plane_state.end(), kOk);
+  h->elev_state = kOk;
+  h->state_state = kOk;
   return tfg_init_state(h);
 }
 
@@ -1391,6 +1550,16 @@ int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int
     std::memcpy(h->in_h[b], src, bytes);
     HIPCHK(h, hipMemcpyAsync(h->in_d[b], h->in_h[b], bytes, hipMemcpyHostToDevice, h->stream));
     dsrc = h->in_d[b];
+  }
+  if (h->engine == TFG_F32) {  // finite-data tracking: host inputs are checked here, device inputs later
+    static const int map[5] = {F_PA, F_Q, F_P, F_T, F_UZ};  // BMI order -> frame planes
+    for (int f = 0; f < 5; ++f) {
+      uint8_t st = kUnknown;
+      if (!src_on_device)
+        st = src_dtype == TFG_F64 ? host_finite(static_cast<const double*>(src) + (size_t)f * n, n)
+                                  : host_finite(static_cast<const float*>(src) + (size_t)f * n, n);
+      h->plane_state[(size_t)frame * kNumForc + map[f]] = st;
+    }
   }
   if (int rc = launch_scatter(h, frame, dsrc, src_dtype, n)) return rc;
   if (b >= 0) HIPCHK(h, hipEventRecord(h->in_ev[b], h->stream));
@@ -1587,14 +1756,21 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
     }
   }
   std::memcpy(h->io_h + u_off, u, sizeof(tfg_uniforms));
+  IoArgs io;
+  if (h->engine == TFG_F32) {  // finite-data status of the step's inputs, as the kernel reads them
+    io.in_state = kOk;
+    for (int f = 0; f < 5; ++f)
+      if (host_finite(reinterpret_cast<const float*>(h->io_h + (size_t)map[f] * np * h->rsz), n) != kOk) io.in_state = kDirty;
+  }
   TFG_TSTAMP(t_in1);
   TFG_TACC(0, t_in0, t_in1);
-  IoArgs io;
   io.in = h->io_d;
   io.out = reinterpret_cast<double*>(h->io_d + out_off);
   io.flag = reinterpret_cast<uint32_t*>(h->io_d + flag_off);
   io.seq = ++h->io_seq == 0 ? ++h->io_seq : h->io_seq;  // never 0, the initial flag value
   if (int rc = launch_steps(h, reinterpret_cast<const tfg_uniforms*>(h->io_d + u_off), u, 1, io)) return rc;
+  if (h->engine == TFG_F32)  // the kernel stored the inputs into the frame
+    std::fill_n(h->plane_state.begin() + (size_t)frame * kNumForc, kNumForc, io.in_state);
   TFG_TSTAMP(t_l1);
   TFG_TACC(1, t_in1, t_l1);
   if (int rc = wait_flags(h, flag_off, blocks, io.seq)) return rc;
@@ -1934,16 +2110,17 @@ int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx,
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
   if (!(k_snow >= 0) || !(k_ice >= 0)) return fail(h, TFG_ERR_ARG, "conductivities must be >= 0");
-  HIPCHK(h, hipSetDevice(h->device));
-  tfg::CondGrid g;
-  if (int rc = cond_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
-  if (int rc = ensure_qc(h)) return rc;
+  // every argument check before cond_setup queues copies from the caller's halo rows
   if (!std::isfinite(q_ground)) return fail(h, TFG_ERR_ARG, "ground heat flux must be finite");
-  const tfg::CondK K = {k_snow / (dx * dx), k_snow / (dy * dy), k_ice * h->h_active / (dx * dx),
-                        k_ice * h->h_active / (dy * dy), q_ground};
   const int64_t gx = (h->nx + tfg::kCondOut - 1) / tfg::kCondOut, strips = (h->ny + tfg::kCondRows - 1) / tfg::kCondRows;
   const int64_t per_xcd = (gx * strips + 7) / 8;
   if (8 * per_xcd > 0x7fffffff) return fail(h, TFG_ERR_ARG, "conduction: grid too large");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (int rc = ensure_qc(h)) return rc;
+  tfg::CondGrid g;
+  if (int rc = cond_setup(h, halo_north, halo_south, halo_on_device, g)) return rc;
+  const tfg::CondK K = {k_snow / (dx * dx), k_snow / (dy * dy), k_ice * h->h_active / (dx * dx),
+                        k_ice * h->h_active / (dy * dy), q_ground};
   if (h->engine == TFG_F32)
     hipLaunchKernelGGL((tfg::k_conduction<float>), (unsigned)(8 * per_xcd), tfg::kCondTX, 0, h->stream, g, K,
                        (float*)h->qc, (int)gx, (int)strips, (int)per_xcd);
@@ -1954,6 +2131,8 @@ int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx,
   // the halo rows are the caller's: finish reading them before returning
   if (halo_north || halo_south) HIPCHK(h, hipStreamSynchronize(h->stream));
   h->qc_on = true;
+  // Qc of a finite state is finite; a neighbour's halo rows are not checked here
+  h->qc_state = (h->state_state == kOk && !halo_north && !halo_south) ? kOk : kUnknown;
   return TFG_OK;
 }
 

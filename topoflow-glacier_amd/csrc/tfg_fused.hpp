@@ -1,5 +1,5 @@
 // tfg_fused.hpp -- the fused multi-step kernel k_fused<R, EXACT, READ_DEPTHS,
-// CATCH, QC, C> and its helpers, shared by the two translation units of the
+// CATCH, QC, C, NS> and its helpers, shared by the two translation units of the
 // engine library: tfg_engine.hip (the C ABI, every other kernel, and the fp32
 // engine's instantiations) and tfg_fused_f64.hip (the fp64 engine's
 // instantiations, compiled with different code-motion flags; see there).
@@ -207,7 +207,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_MIN_WAVES_EXACT
 #define TFG_MIN_WAVES_EXACT 2  // fp64 engine: 256 VGPRs, no scratch spills
 #endif
-template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C>
+// NS (fast engine only): the NaN-safe form of the step (tfg::cell_step_fast),
+// for launches the host could not verify to read only finite values.
+template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false>
 __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
@@ -375,9 +377,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           } else {
             tfg::CellOutF o;
-            tfg::cell_step_fast<QC>(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j],
-                                    (float)f.Q[j], (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j],
-                                    (float)qc[j]);
+            tfg::cell_step_fast<QC, NS>(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j],
+                                        (float)f.Q[j], (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j],
+                                        (float)qc[j]);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           }

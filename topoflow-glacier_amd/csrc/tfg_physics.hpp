@@ -798,19 +798,113 @@ struct CellOutF {
   float h_snow, SM, h_ice, IM, M_total, RH;
 };
 
-template <bool QC>
+// Missing data.  The reference's np.maximum / np.minimum propagate NaN, its
+// P * (T > T_rs) and P * (T <= T_rs) are both 0 for a NaN T_air, and a NaN in
+// the snowfall window freezes n (:1035-1041).  The fast step comes in two
+// forms: NANSAFE = true spells all of that out (npmax / npmin, both rain/snow
+// tests, the window's NaN count), NANSAFE = false uses single-instruction IEEE
+// max / min and plain window arithmetic, which give the same results wherever
+// the step's forcing, statics, state and window hold only finite values.  The
+// host picks the form per launch (tfg_engine.hip, launch_fused): the clean
+// form only when it has verified that a launch reads no non-finite value.
+template <bool NS> __device__ __forceinline__ float nmax(float a, float b) { if constexpr (NS) return npmax(a, b); else return fmaxf(a, b); }
+template <bool NS> __device__ __forceinline__ float nmin(float a, float b) { if constexpr (NS) return npmin(a, b); else return fminf(a, b); }
+template <bool NS> __device__ __forceinline__ double dmax(double a, double b) { if constexpr (NS) return npmax(a, b); else return fmax(a, b); }
+template <bool NS> __device__ __forceinline__ double dmin(double a, double b) { if constexpr (NS) return npmin(a, b); else return fmin(a, b); }
+
+// The fast step's state update (:1566-1731): fp64 where depths and cold
+// contents accumulate.  NANSAFE: max / min as numpy's np.maximum / np.minimum,
+// so missing forcing turns the same outputs NaN as in the reference.  Returns
+// the new state, the clamped melt rates and the two diagnostic terms.
+struct MeltF {
+  double h_swe, h_iwe, Eccs, Ecci;
+  float SM, IM, Erem_s, IM_int;  // outputs; terms of the SM and IM integrals (:1486, :1493)
+};
+template <bool NS>
+__device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, float P_snow, float RH, float T_air,
+                                           double h_swe0, double h_iwe0, double Eccs0, double Ecci0,
+                                           double h_ice_prev) {
+  MeltF m;
+  const double previous_swe = h_swe0;
+  const double E_in = (double)(Q_sum * p.f_dt);
+  // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
+  const double E_rem_s = dmax<NS>(E_in - Eccs0, 0.0);
+  m.Erem_s = (float)E_rem_s;
+  // update_swe (:1594-1606)
+  double h_swe = add_rounded(h_swe0, (double)P_snow, p.dt);
+  const double ts = dmin<NS>(E_rem_s * p.c_sm3600, h_swe);
+  const double SM = ts * (1.0 / 3600.0);
+  h_swe = dmax<NS>(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
+  // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
+  double Eccs = Eccs0;
+  if (P_snow > 0.0f) {
+    const float rh = RH;
+    const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
+                       fast_atanf(rh - 1.676331f) +
+                       (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
+    Eccs = dmax<NS>(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
+  }
+  // ice melt (:1418-1434), cap (:1473-1480), integral (:1493), update_iwe (:1612-1617)
+  const double E_rem_i = dmax<NS>(E_in - Ecci0, 0.0);
+  double IM = (h_swe == 0.0 && previous_swe == 0.0) ? E_rem_i * p.inv_dt_rhoLf : 0.0;
+  double Ecci = dmax<NS>(Ecci0 - E_in, 0.0);
+  Ecci = (h_ice_prev == 0.0) ? 0.0 : Ecci;
+  IM = dmin<NS>(IM, h_iwe0 * p.inv_dt);  // max(IM, 0) is implied (IM, h_iwe >= 0 or NaN)
+  m.IM_int = (float)IM;
+  const double ti = dmin<NS>(IM * 3600.0, h_iwe0);
+  IM = ti * (1.0 / 3600.0);
+  const double h_iwe = dmax<NS>(sub_rounded(h_iwe0, IM, p.dt3600), 0.0);
+  // snowpack cold content (:1556-1558) with the new h_snow = h_swe * ws (> 0
+  // exactly where h_swe > 0); P_snow <= 0 written out in the NaN-safe form:
+  // a NaN snowfall leaves Eccs alone, as np.where does
+  if (NS ? (P_snow <= 0.0f) : !(P_snow > 0.0f)) Eccs = dmax<NS>(Eccs - E_in, 0.0);
+  Eccs = (h_swe * p.ws == 0.0) ? 0.0 : Eccs;
+  m.h_swe = h_swe;
+  m.h_iwe = h_iwe;
+  m.Eccs = Eccs;
+  m.Ecci = Ecci;
+  m.SM = (float)SM;
+  m.IM = (float)IM;
+  return m;
+}
+template <bool NS>
+__device__ __forceinline__ void melt_fast(const DevParams& p, float Q_sum, float P_snow, float P_rain, float RH,
+                                          float T_air, CellState& st, CellOutF& o, DiagF& d) {
+  const MeltF m = melt_core<NS>(p, Q_sum, P_snow, RH, T_air, st.h_swe, st.h_iwe, st.Eccs, st.Ecci, st.h_ice);
+  d.Erem_s += m.Erem_s;
+  d.IM += m.IM_int;
+  // depths (:1711, :1726)
+  const double h_snow = m.h_swe * p.ws;
+  const double h_ice = m.h_iwe * p.wi;
+  st.h_swe = m.h_swe;
+  st.h_iwe = m.h_iwe;
+  st.Eccs = m.Eccs;
+  st.Ecci = m.Ecci;
+  st.h_snow = h_snow;
+  st.h_ice = h_ice;
+  o.h_snow = (float)h_snow;
+  o.h_ice = (float)h_ice;
+  o.SM = m.SM;
+  o.IM = m.IM;
+  o.M_total = m.IM + m.SM + P_rain * (1.0f / 3600.0f);  // :1441-1443
+  o.RH = RH;
+}
+
+template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
                                       const tfg_uniforms& u, const double* __restrict__ geo_d, int64_t n_pad,
                                       int64_t cell, float P, float T_air, float Hum_sp, float P_air, float uz,
                                       int32_t q_old, int32_t& q_new, CellState& st, CellOutF& o, DiagF& d, float qc) {
+  constexpr bool NS = NANSAFE;
   const bool snow_pos = st.h_snow > 0.0, ice_pos = st.h_ice > 0.0;  // previous-step depths
   const float T_K = T_air + 273.15f;
   const float rT = frcp(T_K);
   // rain/snow split (:578-604): T_air > T_rs, exact via the rounded-down
-  // threshold; both tests written out, so a NaN T_air gives P * 0 for both,
-  // as the reference's P * (T > T_rs) and P * (T <= T_rs) do
-  const float P_rain = (T_air > p.f_T_rs_dn) ? P : P * 0.0f;
-  const float P_snow = (T_air <= p.f_T_rs_dn) ? P : P * 0.0f;
+  // threshold; NaN-safe: both tests written out, so a NaN T_air gives P * 0
+  // for both, as the reference's P * (T > T_rs) and P * (T <= T_rs) do
+  const bool is_rain = T_air > p.f_T_rs_dn;
+  const float P_rain = is_rain ? P : P * 0.0f;
+  const float P_snow = (NS ? (T_air <= p.f_T_rs_dn) : !is_rain) ? P : P * 0.0f;
   d.P += P;
   d.Pmax = npmax(d.Pmax, P);
   d.PR += P_rain;
@@ -841,13 +935,13 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float log_term = flog2(e_air) * kLn2 - 1.8102704f;
 #endif
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
-  const float T_surf = (snow_pos || ice_pos) ? npmin(T_dew, 0.0f) : T_dew;
+  const float T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
   // turbulent fluxes (:640-745, :919-934)
   const float dTs = T_air - T_surf;
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
   const float Ri = p.f_gz * dTs * frcp(bot);
-  const float L2 = flog2_split(npmax((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
+  const float L2 = flog2_split(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
   const float Dn = uz * p.f_k2 * frcp(L2 * L2);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
   // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
@@ -872,10 +966,16 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // snowfall window + albedo ageing (:1006-1059)
   {
     const float sq = P_snow * p.f_qfac;  // P_snow*dt*ws*2^36
-    q_new = (sq == sq) ? (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f)) : kWindowNan;
+    const int32_t q = (int32_t)__float2int_rn(fminf(fmaxf(sq, -2147483520.0f), 2147483520.0f));
+    q_new = NS ? ((sq == sq) ? q : kWindowNan) : q;
   }
-  st.tot_q += window_tot(q_new) - window_tot(q_old);
-  st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
+  if constexpr (NS) {
+    st.tot_q += window_tot(q_new) - window_tot(q_old);
+    st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
+  } else {  // no NaN slot in the window (nan_forcing)
+    st.tot_q += (int64_t)q_new - (int64_t)q_old;
+    st.n = (st.tot_q >= p.thr_q) ? 0.0 : st.n + p.days_per_dt;
+  }
   float albedo;
   {
     // selects in fp32: albedo is rebuilt every step from n and the depths
@@ -890,11 +990,13 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   }
   // clear-sky shortwave (SF:904-941); W_p = 1.12*w
   const float w = fexp2((0.0614f * kLog2e) * T_dew);
-  const float tau = npmin(npmax(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);  // SF:614
+  const float tau = nmin<NS>(nmax<NS>(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);  // SF:614
   const float gam_s = p.f_1pdust - fexp2(fmaf(u.gam_c1, w, u.gam_c0));
   // cos(lat_eq)*cos(omega*th + dlon)
   const float cwl = u.cos_wth_f * g.cc - u.sin_wth_f * g.cs;
-  const float K_ET = npmax(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);  // SF:887
+  // SF:887; the geometry planes are never NaN (derive_geo maps a NaN slope or
+  // aspect to the reference's 0), so IEEE max is exact here in both forms
+  const float K_ET = fmaxf(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);
   const float kf = u.k_et_flat_f;
   const float K_dif = 0.5f * gam_s * kf;
   const float K_bs = 0.5f * gam_s * albedo * fmaf(tau, kf, K_dif);
@@ -929,57 +1031,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
   if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
 
-  // ---- state update (:1566-1731), fp64 where depths and cold contents accumulate.
-  // max / min as numpy's np.maximum / np.minimum (NaN-propagating), so missing
-  // forcing turns the same outputs NaN as in the reference
-  const double previous_swe = st.h_swe;
-  const double E_in = (double)(Q_sum * p.f_dt);
-  // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
-  const double E_rem_s = npmax(E_in - st.Eccs, 0.0);
-  d.Erem_s += (float)E_rem_s;
-  // update_swe (:1594-1606)
-  double h_swe = add_rounded(st.h_swe, (double)P_snow, p.dt);
-  const double ts = npmin(E_rem_s * p.c_sm3600, h_swe);
-  const double SM = ts * (1.0 / 3600.0);
-  h_swe = npmax(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
-  // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
-  double Eccs = st.Eccs;
-  if (P_snow > 0.0f) {
-    const float rh = RH;
-    const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
-                       fast_atanf(rh - 1.676331f) +
-                       (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
-    Eccs = npmax(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
-  }
-  // ice melt (:1418-1434), cap (:1473-1480), integral (:1493), update_iwe (:1612-1617)
-  const double E_rem_i = npmax(E_in - st.Ecci, 0.0);
-  double IM = (h_swe == 0.0 && previous_swe == 0.0) ? E_rem_i * p.inv_dt_rhoLf : 0.0;
-  double Ecci = npmax(st.Ecci - E_in, 0.0);
-  Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;
-  IM = npmin(IM, st.h_iwe * p.inv_dt);  // max(IM, 0) is implied (IM, h_iwe >= 0 or NaN)
-  d.IM += (float)IM;
-  const double ti = npmin(IM * 3600.0, st.h_iwe);
-  IM = ti * (1.0 / 3600.0);
-  const double h_iwe = npmax(sub_rounded(st.h_iwe, IM, p.dt3600), 0.0);
-  // depths (:1711, :1726), snowpack cold content (:1556-1558, new h_snow);
-  // P_snow <= 0 written out: a NaN snowfall leaves Eccs alone, as np.where does
-  const double h_snow = h_swe * p.ws;
-  const double h_ice = h_iwe * p.wi;
-  if (P_snow <= 0.0f) Eccs = npmax(Eccs - E_in, 0.0);
-  Eccs = (h_snow == 0.0) ? 0.0 : Eccs;
-  st.h_swe = h_swe;
-  st.h_iwe = h_iwe;
-  st.Eccs = Eccs;
-  st.Ecci = Ecci;
-  st.h_snow = h_snow;
-  st.h_ice = h_ice;
-  const float SMf = (float)SM, IMf = (float)IM;
-  o.h_snow = (float)h_snow;
-  o.h_ice = (float)h_ice;
-  o.SM = SMf;
-  o.IM = IMf;
-  o.M_total = IMf + SMf + P_rain * (1.0f / 3600.0f);  // :1441-1443
-  o.RH = RH;
+  melt_fast<NS>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
 #if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
   const float dbg[13] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
   o.RH = dbg[TFG_DEBUG_TERM];

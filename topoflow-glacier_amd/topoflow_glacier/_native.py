@@ -123,8 +123,11 @@ def load() -> ctypes.CDLL:
         "tfg_conduction_update": ([vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                    ctypes.c_double, dp, dp, i32], i32),
         "tfg_conduction_off": ([vp], i32),
+        "tfg_nan_safe_launches": ([vp, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sigs.items():
+        if "TFG_LIB" in os.environ and not hasattr(L, name):
+            continue  # an older library variant under same-box A/B (scripts/gpu_ab_same_box.sh)
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -162,7 +165,7 @@ def code_object_sha256(path: Path | None = None) -> str | None:
     return hashlib.sha256(blob).hexdigest() if blob else None
 
 
-BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1E"  # k_fused<float, false, false, false, false, 1>
+BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0E"  # k_fused<float, false, false, false, false, 1, false>
 
 
 def gfx950_code_objects(path: Path | None = None) -> list[bytes]:
@@ -284,4 +287,5 @@ def exported_symbols() -> list[str]:
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update", "tfg_update_many", "tfg_conduction_edges", "tfg_conduction_update", "tfg_conduction_off",
+        "tfg_nan_safe_launches",
     ) if hasattr(L, n)]

@@ -277,6 +277,13 @@ class GlacierEngine:
     def sync(self) -> None:
         self._chk(self.lib.tfg_sync(self.h))
 
+    def nan_safe_launches(self) -> int:
+        """Launches that ran the fp32 engine's NaN-safe step form (include/tfg.h,
+        tfg_nan_safe_launches): missing data, or data not known to be finite."""
+        c = ctypes.c_int64()
+        self._chk(self.lib.tfg_nan_safe_launches(self.h, ctypes.byref(c)))
+        return int(c.value)
+
     def set_stream(self, stream_ptr: int | None) -> None:
         self._chk(self.lib.tfg_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)))
         self._stream_ptr = stream_ptr or None
