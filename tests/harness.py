@@ -159,8 +159,13 @@ def melt_out_flips(gpu: dict, ref: dict, rtol: float = 1e-5):
 # SIMD libm, bit-exact to the reference fixtures) -- two fp64 restatements of
 # the same operation order.  Measured ratio GPU fp32 / fp64 baseline: 1.94 on
 # bench.py's sample (4174 / 2149 of 262 144 cells x 96 steps) and 2.0 on the
-# year-long run (ice divergence in 74 / 37 of 2048 cells); DESIGN.md section 3.
-FLIP_RATIO_MAX = 3.0
+# year-long run (ice divergence in 74 / 37 of 2048 cells).  That ratio is the
+# floor for any engine whose Q_sum differs from numpy's in the last bit: the
+# oracle with Q_sum perturbed by a relative 3e-7 ... 1e-15 flips 1.86-1.91 x the
+# baseline, and an exact Q_sum near the melt gates changes nothing
+# (tests/diagnostics/melt_gate_flips.py, profiles/r3_melt_gate_flips.json;
+# DESIGN.md section 3).  The budget is that ratio plus margin.
+FLIP_RATIO_MAX = 2.5
 FLIP_SLACK = 3  # absolute allowance for samples whose baseline is a handful of cells
 
 
