@@ -27,9 +27,10 @@ Fixtures written (all small .npz, float64):
 * ``satterlund.npz`` -- SATTERLUND = True (the alternative vapour-pressure and
   emissivity formulas).
 * ``params.npz`` -- non-default dust_atten / canopy_factor / cloud_factor.
-* ``clock_phoenix.npz``, ``clock_anchorage.npz`` -- runs outside
-  America/Los_Angeles across a DST change (central Arizona, no DST; Wolverine
-  Glacier, Alaska), carrying the zone name the timezonefinder stub returned.
+* ``clock_<zone>.npz`` (phoenix, anchorage, denver, boise, chicago, new_york,
+  honolulu) -- runs outside America/Los_Angeles across a US DST change, one
+  interior point of every other zone the build's lat/lon table returns,
+  carrying the zone name the timezonefinder stub returned.
 
 Usage:  python3 tests/golden/make_golden.py   (takes ~1 minute)
         python3 tests/golden/make_golden.py --only satterlund,params,zones
@@ -61,18 +62,25 @@ SHIMS = {
     """,
     # timezonefinder's polygon data is not available offline.  The stub answers
     # what its polygons give for the points the fixtures use: the Pacific
-    # Northwest box (every reference config), central Arizona (34.0 N,
-    # 111.5 W: America/Phoenix, no DST) and Wolverine Glacier, Alaska
-    # (60.4 N, 148.9 W: America/Anchorage).
+    # Northwest box (every reference config), and one interior point per other
+    # zone the build's table (physics/clock.py) can return: central Arizona
+    # (34.0 N, 111.5 W: America/Phoenix, no DST), Wolverine Glacier, Alaska
+    # (60.4 N, 148.9 W), Arapaho Glacier, Colorado (40.02 N, 105.65 W), the
+    # Sawtooth Range, Idaho (44.1 N, 114.9 W), central Iowa (41.9 N, 93.1 W),
+    # Mount Washington, New Hampshire (44.27 N, 71.3 W) and Mauna Kea, Hawaii
+    # (19.82 N, 155.47 W).
     "timezonefinder.py": """
+        POINTS = {(34.0, -111.5): "America/Phoenix", (60.4, -148.9): "America/Anchorage",
+                  (40.02, -105.65): "America/Denver", (44.1, -114.9): "America/Boise",
+                  (41.9, -93.1): "America/Chicago", (44.27, -71.3): "America/New_York",
+                  (19.82, -155.47): "Pacific/Honolulu"}
         class TimezoneFinder:
             def timezone_at(self, lat=None, lng=None):
-                if -125 <= lng <= -114 and 32 <= lat <= 49.5:
+                if -125 <= lng <= -114 and 32 <= lat <= 49.5 and not (abs(lat - 44.1) < 0.01 and abs(lng + 114.9) < 0.01):
                     return "America/Los_Angeles"
-                if abs(lat - 34.0) < 0.01 and abs(lng + 111.5) < 0.01:
-                    return "America/Phoenix"
-                if abs(lat - 60.4) < 0.01 and abs(lng + 148.9) < 0.01:
-                    return "America/Anchorage"
+                for (la, lo), zone in POINTS.items():
+                    if abs(lat - la) < 0.01 and abs(lng - lo) < 0.01:
+                        return zone
                 return None
             def certain_timezone_at(self, lat=None, lng=None):
                 return self.timezone_at(lat=lat, lng=lng)
@@ -313,6 +321,11 @@ def build_clock_windows():
 ZONE_WINDOWS = (  # (tag, lat, lon, zone the stub returns, start, steps): each crosses a US DST change
     ("phoenix", 34.0, -111.5, "America/Phoenix", "2014030712", 96),
     ("anchorage", 60.4, -148.9, "America/Anchorage", "2013110112", 96),
+    ("denver", 40.02, -105.65, "America/Denver", "2014030712", 96),
+    ("boise", 44.1, -114.9, "America/Boise", "2013110112", 96),
+    ("chicago", 41.9, -93.1, "America/Chicago", "2014030712", 96),
+    ("new_york", 44.27, -71.3, "America/New_York", "2013110112", 96),
+    ("honolulu", 19.82, -155.47, "Pacific/Honolulu", "2013110112", 96),  # no DST: the offset stays -10
 )
 
 

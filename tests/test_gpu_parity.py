@@ -157,7 +157,8 @@ def test_update_until_equals_repeated_update(tmp_path):
 
 # ---------------------------------------------------------------- engines vs reference fixtures
 @pytest.mark.parametrize("name", ["grid64", "dt2", "dt_quarter", "clock_dst_end", "clock_dst_start", "clock_new_year",
-                                  "satterlund", "params", "clock_phoenix", "clock_anchorage"])
+                                  "satterlund", "params", "clock_phoenix", "clock_anchorage", "clock_denver",
+                                  "clock_boise", "clock_chicago", "clock_new_york", "clock_honolulu"])
 def test_fp64_engine_vs_reference_fixtures(name):
     g = load_golden(name)
     n = g["ncell"]

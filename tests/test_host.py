@@ -18,11 +18,14 @@ import tfg_oracle as O  # noqa: E402  (checker)
 
 # ----------------------------------------------------------------- clock
 @pytest.mark.parametrize("name", ["cat3062920_265", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2",
-                                  "dt_quarter", "clock_phoenix", "clock_anchorage"])
+                                  "dt_quarter", "clock_phoenix", "clock_anchorage", "clock_denver", "clock_boise",
+                                  "clock_chicago", "clock_new_york", "clock_honolulu"])
 def test_clock_matches_reference(name):
     """The model clock (zone from lat/lon via zone_for) against the reference's
-    own clock: Pacific across DST changes and the year end, Arizona (no DST)
-    across the DST start, Alaska across the DST end."""
+    own clock: Pacific across DST changes and the year end, and one point of
+    every other zone the table returns across a DST change -- Arizona (no DST)
+    and Denver, Chicago across the DST start; Alaska, Boise, New York and
+    Hawaii (no DST) across the DST end."""
     from topoflow_glacier.physics.clock import StepClock, zone_for
 
     g = load_golden(name)
@@ -33,6 +36,29 @@ def test_clock_matches_reference(name):
     assert np.array_equal(jd, g["internal"]["julian_day"][:, 0])
     assert np.array_equal(gmt, g["internal"]["GMT_offset"][:, 0])
     assert np.array_equal(tsn, g["internal"]["TSN_offset"][:, 0])  # bit-exact
+
+
+@pytest.mark.parametrize("lat,lon,zone", [
+    (34.0, -103.08, "America/Denver"), (34.0, -103.06, None),    # New Mexico / the Texas strip (103.064 W)
+    (43.5, -116.95, "America/Boise"), (44.5, -116.75, "America/Boise"),
+    (44.5, -116.9, None), (44.9, -116.75, None),                  # Baker County, Oregon (Pacific) across the Snake
+    (42.5, -117.1, None),                                         # Malheur County west of the box
+    (37.5, -114.0, "America/Denver"), (37.5, -114.1, "America/Los_Angeles"),  # Utah / Nevada
+    (36.0, -112.1, "America/Phoenix"), (36.0, -111.9, None),      # the Navajo Nation (DST) stays out
+    (44.0, -88.6, "America/Chicago"), (44.0, -88.4, None),        # Wisconsin / Lake Michigan's Central-Eastern gap
+    (43.7, -79.4, "America/New_York"),                            # Toronto: America/Toronto, the same offsets
+    (61.0, -140.9, None), (61.0, -141.1, "America/Anchorage"),    # Yukon / Alaska
+])
+def test_zone_table_edges(lat, lon, zone):
+    """Points just inside and just outside the zone boxes' edges
+    (physics/clock.py _ZONES): a box never reaches across a zone line."""
+    from topoflow_glacier.physics.clock import zone_for
+
+    if zone is None:
+        with pytest.raises(ValueError):
+            zone_for(lat, lon)
+    else:
+        assert zone_for(lat, lon) == zone
 
 
 def test_uniforms_match_oracle_functions():

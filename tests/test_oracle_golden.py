@@ -8,7 +8,8 @@ import pytest
 from tests.harness import GOLDEN, OUT_NAMES, load_golden, oracle_run
 
 FIXTURES = ["cat3062920_265", "grid64", "clock_dst_end", "clock_dst_start", "clock_new_year", "dt2", "dt_quarter",
-            "satterlund", "params", "clock_phoenix", "clock_anchorage"]
+            "satterlund", "params", "clock_phoenix", "clock_anchorage", "clock_denver", "clock_boise", "clock_chicago",
+            "clock_new_york", "clock_honolulu"]
 RTOL = 1e-12  # bit-exact here; margin for numpy SIMD paths of other host CPUs
 
 

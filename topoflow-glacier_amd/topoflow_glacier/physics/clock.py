@@ -41,9 +41,11 @@ _TP = (
 PERIHELION = {1981 + i: tuple(int(x) for x in v.split(":")) for i, v in enumerate(_TP.split())}
 
 # IANA zones by lat/lon box, for points where a box can be justified: every
-# box lies wholly inside ONE zone's territory (borders and the water or
-# neighbouring country beyond them included), so a point in it can only be in
-# that zone.  Where zones meet irregularly -- the Idaho and Oregon Pacific /
+# box lies wholly inside territory with ONE set of UTC offsets (borders and the
+# water beyond them included), so a point in it gets the offsets the
+# reference's timezonefinder + zoneinfo lookup gives.  The zone name is that of
+# the US territory; the Eastern box also covers southern Ontario, whose
+# America/Toronto has the same offsets and DST dates as America/New_York.  Where zones meet irregularly -- the Idaho and Oregon Pacific /
 # Mountain line, the Navajo Nation (DST) inside Arizona (no DST), the Alaska
 # panhandle against British Columbia and Yukon, the Central / Eastern line,
 # Indiana -- no box reaches, and the caller must set `time_zone`.  The
@@ -62,13 +64,16 @@ _ZONES = [
     ((37.0, 42.0, -114.05, -109.05), "America/Denver"),
     ((37.0, 41.0, -109.05, -102.05), "America/Denver"),
     ((41.0, 45.0, -111.05, -104.05), "America/Denver"),
-    ((32.0, 37.0, -109.05, -103.0), "America/Denver"),
+    ((32.0, 37.0, -109.05, -103.07), "America/Denver"),  # clear of the Texas line at 103.064 W
     ((31.79, 32.0, -109.05, -106.65), "America/Denver"),  # southern New Mexico, clear of Chihuahua
     # Mountain, DST: Montana east of the Bitterroot divide, and north of 48 N east of the 116.05 W line
     ((45.0, 49.0, -113.0, -104.05), "America/Denver"),
     ((48.0, 49.0, -116.0, -104.05), "America/Denver"),
-    # Mountain, DST: southern Idaho and Malheur County, Oregon
-    ((42.0, 44.8, -117.0, -111.05), "America/Boise"),
+    # Mountain, DST: southern Idaho and Malheur County, Oregon (the state line at
+    # 117.03 W up to the Snake's mouth of the Owyhee, 43.8 N); north of 43.8 N the
+    # box stays east of the Snake River, beyond which Baker County, Oregon keeps Pacific time
+    ((42.0, 43.8, -117.0, -111.05), "America/Boise"),
+    ((43.8, 44.8, -116.8, -111.05), "America/Boise"),
     # Arizona outside the Navajo Nation: Mountain, no DST
     ((31.34, 34.8, -111.0, -109.05), "America/Phoenix"),
     ((32.5, 35.0, -114.0, -111.0), "America/Phoenix"),
