@@ -280,6 +280,13 @@ int tfg_sync(tfg_handle* h);
  * The environment variable TFG_NANSAFE=1 at tfg_create forces that form. */
 int tfg_nan_safe_launches(tfg_handle* h, int64_t* count);
 
+/* Self-test of the fp64 engine's power rewrites on the device (tests only):
+ * out[i] = pow4(x[i]) (which = 0: T^4, :1231-1233), pow1p5(x[i]) (1: RH^1.5,
+ * :1520) or exp(log(x[i]) / 7) (2: em_air's 1/7 power, :1167), computed by the
+ * same device functions the engine's steps call.  Host arrays of n values,
+ * synchronous. */
+int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out);
+
 /* Device-side synthetic workload generator (bench / tests): fills the forcing
  * frames, static rasters and initial depths from a counter-based hash of
  * (seed, field, frame, global cell index).  `row0` is this shard's first row in

@@ -303,3 +303,39 @@ def test_deferred_updates_equal_per_model_updates(tmp_path, monkeypatch):
         update_many([e._engine, e._engine], [e._in_block] * 2, [e._out_block] * 2)
     assert e._engine.step_index == k  # no step ran
     e.finalize()
+
+
+@pytest.mark.gpu
+def test_deferred_update_uses_the_inputs_update_was_given(tmp_path):
+    """``defer_update``: update() copies the step's five inputs when it queues
+    the step.  A write through a get_value_ptr view between update() and the
+    flush changes the NEXT step, not the queued one, as in the reference, whose
+    update() uses its inputs at once."""
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    cfg_d, cfg_n = tmp_path / "d.yaml", tmp_path / "n.yaml"
+    cfg_d.write_text(yaml.dump(dict(BASE_CFG, defer_update=True)))
+    cfg_n.write_text(yaml.dump(BASE_CFG))
+    models = []
+    for c in (cfg_d, cfg_n):
+        m = BmiTopoflowGlacier()
+        m.initialize(str(c))
+        for name, v in (("atmosphere_water__liquid_equivalent_precipitation_rate", 2e-4),
+                        ("land_surface_air__temperature", -1.5), ("land_surface_air__pressure", 88000.0),
+                        ("atmosphere_air_water~vapor__relative_saturation", 0.004), ("wind_speed_UV", 3.0)):
+            m.set_value(name, np.array([v]))
+        models.append(m)
+    d, n = models
+    d.update()  # queued
+    d.get_value_ptr("land_surface_air__temperature")[:] = 25.0  # after update(), before the flush
+    n.update()
+    outs = ("snowpack__melt_volume_flux", "snowpack__liquid-equivalent_depth", "land_surface_water__runoff_volume_flux")
+    for name in outs:  # the first read flushes the queued step
+        assert d.get_value(name, np.zeros(1)).item() == n.get_value(name, np.zeros(1)).item(), name
+    n.set_value("land_surface_air__temperature", np.array([25.0]))
+    d.update()
+    n.update()
+    for name in outs:
+        assert d.get_value(name, np.zeros(1)).item() == n.get_value(name, np.zeros(1)).item(), name
+    for m in models:
+        m.finalize()

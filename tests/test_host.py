@@ -356,9 +356,11 @@ def test_bmi_one_cell_path_does_not_need_torch():
 def test_update_batch_passes_each_queued_step_and_rolls_back_on_error():
     """engine.UpdateBatch / BMI flush_updates without a GPU (a stand-in library
     in place of tfg_update_many): the call gets every queued engine's handle,
-    input, uniform and output addresses in queue order; on an error no step
-    counts, the engines' step counters and the BMI clocks roll back, and every
-    batch has been taken off the queue."""
+    uniform and output addresses in queue order, and the inputs as they were
+    when the step was queued (copied into the batch's own block: a later write
+    into the caller's block does not reach the queued step); on an error no
+    step counts, the engines' step counters and the BMI clocks roll back, and
+    every batch has been taken off the queue."""
     import ctypes
     import types
 
@@ -372,7 +374,8 @@ def test_update_batch_passes_each_queued_step_and_rolls_back_on_error():
         rc = nat.OK
 
         def tfg_update_many(self, hs, m, src, u, dst):
-            calls.append([[a[i] for i in range(m)] for a in (hs, src, u, dst)])
+            staged = [list((ctypes.c_double * 5).from_address(src[i])) for i in range(m)]
+            calls.append([[a[i] for i in range(m)] for a in (hs, u, dst)] + [staged])
             return self.rc
 
     lib = Lib()
@@ -387,15 +390,18 @@ def test_update_batch_passes_each_queued_step_and_rolls_back_on_error():
             return 0, 9000 + self.h.value, None
 
     e1, e2 = Eng(100), Eng(200)
+    v1, v2 = np.arange(5.0), np.arange(5.0) + 10.0
     b = UpdateBatch()
-    b.add_addresses(e1, 11, 21)
-    b.add_addresses(e2, 12, 22)
+    b.add_addresses(e1, v1.ctypes.data, 21)
+    b.add_addresses(e2, v2.ctypes.data, 22)
+    v1[:] = -1.0  # written after the step was queued
     assert len(b) == 2 and (e1.step_index, e2.step_index) == (8, 8)
     b.run()
-    assert calls[-1] == [[100, 200], [11, 12], [9100, 9200], [21, 22]] and len(b) == 0
+    assert calls[-1] == [[100, 200], [9100, 9200], [21, 22], [list(np.arange(5.0)), list(np.arange(5.0) + 10.0)]]
+    assert len(b) == 0
     lib.rc = nat.ERR_ARG
     m1 = types.SimpleNamespace(_queued=True, _timestep=8)
-    b.add_addresses(e1, 11, 21, m1)
+    b.add_addresses(e1, v1.ctypes.data, 21, m1)
     B._BATCHES[("dev", 0)] = b
     with pytest.raises(nat.NativeError):
         B.flush_updates()

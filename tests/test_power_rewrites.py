@@ -12,6 +12,7 @@ itself at 1e-10 and report ~1e-14.
 """
 
 import numpy as np
+import pytest
 
 
 def _ulps(a, b):
@@ -44,3 +45,47 @@ def test_seventh_root_as_exp_log():
         zero, neg = np.float64(0.0), np.float64(-1.0)
         assert np.exp(np.log(zero) * inv7) == zero ** inv7 == 0.0
         assert np.isnan(np.exp(np.log(neg) * inv7)) and np.isnan(neg ** inv7)
+
+
+def _device(x, which):
+    """The engine's own device functions (tfg_selftest_powers: pow4, pow1p5,
+    pow_small_root of csrc/tfg_physics.hpp) on x."""
+    import ctypes
+
+    from topoflow_glacier import _native
+
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    _native.check(_native.load().tfg_selftest_powers(0, x.ctypes.data_as(ctypes.c_void_p), x.size, which,
+                                                     out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+@pytest.mark.gpu
+def test_power_rewrites_on_the_device():
+    """The same three rewrites as run by the GPU (device libm: ocml exp, log and
+    sqrt), against numpy's `**` over the same ranges, with the same bounds, and
+    the same zero and NaN cases."""
+    rng = np.random.default_rng(7)
+    T = rng.uniform(200.0, 330.0, 200_000)
+    assert _ulps(_device(T, 0), T ** 4.0).max() <= 2.0
+    RH = np.concatenate([rng.uniform(0.0, 1.5, 200_000), [0.0, 1.0]])
+    ref = RH ** 1.5
+    got = _device(RH, 1)
+    ok = ref > 0
+    assert _ulps(got[ok], ref[ok]).max() <= 2.0 and got[~ok].tolist() == ref[~ok].tolist()
+    x = (rng.uniform(0.1, 60.0, 200_000) / 10.0) / rng.uniform(200.0, 330.0, 200_000)
+    assert _ulps(_device(x, 2), x ** (1.0 / 7.0)).max() <= 4.0
+    edge = _device(np.array([0.0, -1.0, np.nan]), 2)
+    assert edge[0] == 0.0 and np.isnan(edge[1]) and np.isnan(edge[2])
+    m = {"pow4_max_ulps": float(_ulps(_device(T, 0), T ** 4.0).max()),
+         "pow1p5_max_ulps": float(_ulps(got[ok], ref[ok]).max()),
+         "root7_max_ulps": float(_ulps(_device(x, 2), x ** (1.0 / 7.0)).max())}
+    import json
+    import os
+
+    d = os.environ.get("TFG_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, "power_rewrites_device.json"), "w") as f:
+            json.dump(m, f)

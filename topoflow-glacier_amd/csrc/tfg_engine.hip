@@ -551,6 +551,13 @@ __global__ void k_window_nan(const int64_t* __restrict__ tot, int64_t n, int32_t
 
 enum : uint8_t { kUnknown = 0, kOk = 1, kDirty = 2 };
 
+// tfg_selftest_powers: the fp64 engine's power rewrites (tfg_physics.hpp) on device
+__global__ void k_selftest_powers(const double* __restrict__ x, double* __restrict__ y, int64_t n, int which) {
+  const double inv7 = 1.0 / 7.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = which == 0 ? tfg::pow4(x[i]) : which == 1 ? tfg::pow1p5(x[i]) : tfg::pow_small_root(x[i], inv7);
+}
+
 struct tfg_handle {
   int device = 0, engine = TFG_F32;
   int64_t ny = 0, nx = 0, n = 0, n_pad = 0;
@@ -1474,6 +1481,23 @@ int tfg_reset_diag(tfg_handle* h) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemsetAsync(h->slab, 0, (size_t)h->max_blocks * h->n_catch * 6 * 8, h->stream));
+  return TFG_OK;
+}
+
+int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out) {
+  if (!x || !out || n < 0 || which < 0 || which > 2) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  if (n == 0) return TFG_OK;
+  HIPCHK(nullptr, hipSetDevice(device));
+  double* d = nullptr;
+  HIPCHK(nullptr, hipMalloc((void**)&d, (size_t)n * 16));
+  hipError_t e = hipMemcpy(d, x, (size_t)n * 8, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_selftest_powers, grid_for(n), 256, 0, nullptr, d, d + n, n, which);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d + n, (size_t)n * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(nullptr, TFG_ERR_HIP, std::string("tfg_selftest_powers: ") + hipGetErrorString(e));
   return TFG_OK;
 }
 

@@ -124,6 +124,7 @@ def load() -> ctypes.CDLL:
                                    ctypes.c_double, dp, dp, i32], i32),
         "tfg_conduction_off": ([vp], i32),
         "tfg_nan_safe_launches": ([vp, ctypes.POINTER(i64)], i32),
+        "tfg_selftest_powers": ([i32, vp, i64, i32, vp], i32),
     }
     for name, (args, res) in sigs.items():
         if "TFG_LIB" in os.environ and not hasattr(L, name):
@@ -287,5 +288,5 @@ def exported_symbols() -> list[str]:
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update", "tfg_update_many", "tfg_conduction_edges", "tfg_conduction_update", "tfg_conduction_off",
-        "tfg_nan_safe_launches",
+        "tfg_nan_safe_launches", "tfg_selftest_powers",
     ) if hasattr(L, n)]

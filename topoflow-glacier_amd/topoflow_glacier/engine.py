@@ -454,10 +454,13 @@ class UpdateBatch:
     ``update_io`` calls bit for bit.  An engine may be queued once per run,
     and must not be closed while queued (the BMI flushes before finalize)."""
 
-    __slots__ = ("engines", "h", "src", "u", "dst", "keep", "owners")
+    __slots__ = ("engines", "h", "src", "u", "dst", "keep", "owners", "inputs", "n_in")
+
+    _BLOCK = 256  # input rows per staging block
 
     def __init__(self):
         self.engines, self.h, self.src, self.u, self.dst, self.keep, self.owners = [], [], [], [], [], [], []
+        self.inputs, self.n_in = [], 0  # staging blocks [256][5] float64: the queued steps' inputs
 
     def __len__(self) -> int:
         return len(self.h)
@@ -477,11 +480,20 @@ class UpdateBatch:
 
     def add_addresses(self, e: GlacierEngine, src_addr: int, dst_addr: int, owner=None) -> None:
         """add() for a caller that owns fixed, checked blocks (the BMI's input
-        and output blocks) and passes their addresses."""
+        and output blocks) and passes their addresses.  The five inputs are
+        copied now, into a block the batch owns: the step runs on the values
+        update() was given, whatever the caller writes into its own block (a
+        get_value_ptr view, say) before the batch runs."""
         _frame, uptr, rec = e._next_uniform()
+        row = self.n_in % self._BLOCK
+        if row == 0:
+            self.inputs.append(np.empty((self._BLOCK, 5), dtype=np.float64))
+        blk = self.inputs[-1]
+        ctypes.memmove(blk.ctypes.data + row * 40, src_addr, 40)
+        self.n_in += 1
         self.engines.append(e)
         self.h.append(e.h.value)
-        self.src.append(src_addr)
+        self.src.append(blk.ctypes.data + row * 40)
         self.u.append(uptr)
         self.dst.append(dst_addr)
         self.keep.append(rec)
@@ -504,6 +516,7 @@ class UpdateBatch:
             raise
         finally:
             self.engines, self.h, self.src, self.u, self.dst, self.keep, self.owners = [], [], [], [], [], [], []
+            self.inputs, self.n_in = [], 0
 
 
 def update_many(engines, values, outs) -> None:
