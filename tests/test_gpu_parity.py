@@ -855,3 +855,44 @@ def test_fp32_step_forms_agree_on_finite_data_and_the_engine_picks_them(monkeypa
         assert np.isnan(e.get_field("Eccs")[5]) and np.isfinite(np.delete(e.get_field("Eccs"), 5)).all()
     finally:
         e.close()
+
+
+def test_fp32_form_choice_checks_unknown_data_once():
+    """Data of unknown finite-data status (inputs set from device memory) sends
+    a short launch to the NaN-safe form; a launch of 8 or more steps checks the
+    state first (padding cells of a ragged grid excluded: they are computed
+    from zero inputs) and runs the clean form.  The results equal a run that
+    was clean throughout, bit for bit."""
+    import ctypes
+
+    import torch
+
+    from topoflow_glacier import _native as nat
+    from topoflow_glacier.synthetic import diurnal_table
+
+    ny, nx, seed = 5, 13, 3  # 65 cells, padded to 128
+    runs = []
+    for device_inputs in (False, True):
+        e = make_engine(BASE_CFG, ny, nx, "float32", n_frames=24, hist_depth=32, fuse_steps=32)
+        try:
+            e.fill_synthetic(seed, diurnal_table(24))
+            vals = np.stack([e.get_field(v, index=0) for v in ("P_air", "Hum_sp", "P", "T_air", "uz")])
+            if device_inputs:
+                d = torch.as_tensor(vals, device="cuda:0").contiguous()
+                torch.cuda.synchronize()
+                e._chk(e.lib.tfg_set_inputs(e.h, 0, ctypes.c_void_p(d.data_ptr()), nat.F64, e.n, 1))
+            else:
+                e.set_inputs(vals, 0)
+            e.run(1, frames=np.zeros(1, dtype=np.int32))
+            after_short = e.nan_safe_launches()
+            e.run(32, frames=(np.arange(32, dtype=np.int32) % 23) + 1)
+            e.sync()
+            runs.append(({v: e.get_field(v) for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")},
+                         e.get_outputs(), after_short, e.nan_safe_launches()))
+        finally:
+            e.close()
+    (sa, oa, a1, a2), (sb, ob, b1, b2) = runs
+    assert (a1, a2) == (0, 0) and (b1, b2) == (1, 1)
+    for v in sa:
+        np.testing.assert_array_equal(sa[v], sb[v], err_msg=v)
+    np.testing.assert_array_equal(oa, ob)

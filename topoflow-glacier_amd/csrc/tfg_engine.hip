@@ -535,11 +535,14 @@ __global__ void k_window_total(int64_t* __restrict__ tot, const int32_t* __restr
 // Non-finite checks behind the fp32 engine's choice of step form (see
 // tfg_handle::plane_state): flag |= 1 where a value is NaN or infinite, or
 // where a window total holds a NaN slot.
+// Planes of n cells at a stride of `stride` elements (padding cells excluded:
+// they are computed along, from zero inputs, and may hold anything).
 template <class T>
-__global__ void k_nonfinite(const T* __restrict__ p, int64_t n, int32_t* __restrict__ flag) {
+__global__ void k_nonfinite(const T* __restrict__ p, int64_t n, int64_t stride, int planes, int32_t* __restrict__ flag) {
   bool bad = false;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    bad |= !isfinite(p[i]);
+  for (int k = 0; k < planes; ++k)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+      bad |= !isfinite(p[k * stride + i]);
   if (bad) atomicOr(flag, 1);
 }
 __global__ void k_window_nan(const int64_t* __restrict__ tot, int64_t n, int32_t* __restrict__ flag) {
@@ -699,14 +702,14 @@ int upload(tfg_handle* h, void* dst, int dt, const void* src, int st, int64_t n,
   return TFG_OK;
 }
 
-// kOk when every one of `count` values at device pointer p is finite, kDirty
-// otherwise (synchronous).
-int check_finite(tfg_handle* h, const void* p, int dtype, int64_t count, uint8_t* out) {
+// kOk when every value of `planes` planes of n cells (stride `stride`
+// elements) at device pointer p is finite, kDirty otherwise (synchronous).
+int check_finite(tfg_handle* h, const void* p, int dtype, int64_t n, uint8_t* out, int planes = 1, int64_t stride = 0) {
   HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
   if (dtype == TFG_F64)
-    hipLaunchKernelGGL((k_nonfinite<double>), grid_for(count), 256, 0, h->stream, (const double*)p, count, h->d_flag);
+    hipLaunchKernelGGL((k_nonfinite<double>), grid_for(n), 256, 0, h->stream, (const double*)p, n, stride, planes, h->d_flag);
   else
-    hipLaunchKernelGGL((k_nonfinite<float>), grid_for(count), 256, 0, h->stream, (const float*)p, count, h->d_flag);
+    hipLaunchKernelGGL((k_nonfinite<float>), grid_for(n), 256, 0, h->stream, (const float*)p, n, stride, planes, h->d_flag);
   HIPCHK(h, hipGetLastError());
   int32_t flag = 0;
   HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
@@ -979,6 +982,9 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->nx = nx;
   h->n = ny * nx;
   h->n_pad = round_up(h->n, 64);
+  // TFG_PLANE_SKEW (measurement only): plane stride n_pad + skew cells, so that
+  // the planes of a power-of-two shard do not sit at power-of-two distances
+  if (const char* e = std::getenv("TFG_PLANE_SKEW")) h->n_pad += round_up(std::max<int64_t>(0, atoll(e)), 64);
   if (h->n_pad * 8 >= (int64_t)1 << 32) {
     h->err = "shard too large: ny*nx must stay below 2^29 cells per device (32-bit field offsets)";
     g_err = h->err;
@@ -1338,10 +1344,10 @@ constexpr int kVerifySteps = 8;
 // (after prepare_steps has rebuilt them).  Synchronous.
 int check_state(tfg_handle* h) {
   uint8_t st = kOk;
-  if (int rc = check_finite(h, h->st, TFG_F64, (int64_t)kNumState * h->n_pad, &st)) return rc;
+  if (int rc = check_finite(h, h->st, TFG_F64, h->n, &st, kNumState, h->n_pad)) return rc;
   if (st == kOk) {
     HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
-    hipLaunchKernelGGL(k_window_nan, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->n_pad, h->d_flag);
+    hipLaunchKernelGGL(k_window_nan, grid_for(h->n), 256, 0, h->stream, h->tot, h->n, h->d_flag);
     HIPCHK(h, hipGetLastError());
     int32_t flag = 0;
     HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
