@@ -62,7 +62,11 @@ def launch_bytes_per_cell(fuse: int) -> int:
     LDS cost 8 % of throughput on its own: DESIGN.md section 5.)"""
     return BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH
 
-MIN_LAUNCHES = 3
+MIN_LAUNCHES = 6
+# Why 6: the first launch after the barrier that opens the timed region runs
+# 0.5-3.6 ms long at every shape and warm-up length (profiles/r3c_slab_skew_study.jsonl,
+# profiles/r3f_slab_depth_study.jsonl); over 6 launches it weighs ~1 % on the
+# 1024 x 8192 slab instead of ~2 % over 3 (DESIGN.md section 6).
 # auto launch depth: 96 steps for shards above 2^25 cells (the 8192^2 grid: the
 # 96 output slots already take 155 GB of HBM), 192 below (the strong-scaling
 # slabs: a deeper launch amortises the state-in / state-out phases of each
@@ -476,7 +480,8 @@ def main():
             "steps_note": None if steps == args.steps else (
                 f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps) to cover the "
                 f"{args.steps} requested: a launch keeps each cell's state in registers across its steps, so the "
-                f"timed region is a whole number of launches, at least {MIN_LAUNCHES}"
+                f"timed region is a whole number of launches, at least {MIN_LAUNCHES} (so that the slow first launch after "
+                f"the opening barrier weighs ~1 %)"
                 + ("" if fuse_explicit else f", and a multiple of {STEP_QUANTUM} steps so that every GPU count "
                                             f"times the same work")),
             "launches": {"count": n_launch, "steps_each": args.fuse, "ms_min": float(launch_ms.min()),

@@ -1,0 +1,23 @@
+// Host build of the fp64 engine's exp / log / constant-divisor division
+// (topoflow-glacier_amd/csrc/tfg_fastmath.hpp) for tests/test_fastmath.py:
+// the same source the device compiles, with std::fma for the scalar-operand
+// FMAs.  Built by the test with g++ -O2 -ffp-contract=off (test infrastructure).
+#include "../../topoflow-glacier_amd/csrc/tfg_fastmath.hpp"
+
+extern "C" void fm_eval(const double* x, double* y, long n, int which) {
+  for (long i = 0; i < n; ++i) {
+    const double v = x[i];
+    switch (which) {
+      case 3: y[i] = tfg_fm::exp_k(v); break;
+      case 5: y[i] = tfg_fm::log_k(v); break;
+      case 7: y[i] = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
+      case 8: y[i] = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
+      default: y[i] = 0.0; break;
+    }
+  }
+}
+
+// div_k(x[i], c[i], RN(1/c[i])) for arbitrary divisors
+extern "C" void fm_div(const double* x, const double* c, double* y, long n) {
+  for (long i = 0; i < n; ++i) y[i] = tfg_fm::div_k(x[i], c[i], 1.0 / c[i]);
+}

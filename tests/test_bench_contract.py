@@ -39,14 +39,14 @@ def test_default_shard_plan_is_config4_strong_scaling(world):
 
 @pytest.mark.parametrize("world,fuse", [(1, 96), (2, 192), (4, 192), (8, 192)])
 def test_driver_command_times_the_same_work_at_every_n(world, fuse):
-    """`--steps 20`: whole launches, >= 3, and the same 576 steps at every N
+    """`--steps 20`: whole launches, >= 6, and the same 1152 steps at every N
     (96-step launches for the whole 8192^2 grid, 192-step ones for the slabs)."""
     bench, args = _args("--gpus", str(world), "--steps", "20", "--warmup", "5")
     plan = bench.shard_plan(args, world, 0)
     k = bench.auto_fuse(plan["rows_max"] * args.nx)
     steps = bench.timed_steps(args.steps, k, explicit=False)
-    assert k == fuse and steps == 576 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
-    assert bench.timed_steps(48, 24, explicit=True) == 72  # an explicit --fuse: >= 3 launches of it
+    assert k == fuse and steps == 1152 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
+    assert bench.timed_steps(48, 24, explicit=True) == 144  # an explicit --fuse: >= 6 launches of it
     # the driver's --warmup 5 still warms one whole launch of the timed depth
     assert bench.warmup_steps(args.warmup, k) == k and bench.warmup_steps(400, k) == 400
 
@@ -70,9 +70,9 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
         assert k in d, k
-    # --steps 48 with 24-step launches: at least 3 whole launches are timed
-    assert d["n_gpus"] == 1 and d["steps"] == 72 and d["steps_requested"] == 48 and d["steps_note"]
-    assert d["launches"]["count"] == 3 and d["launches"]["ms_min"] <= d["launches"]["ms_mean"] <= d["launches"]["ms_max"]
+    # --steps 48 with 24-step launches: at least 6 whole launches are timed
+    assert d["n_gpus"] == 1 and d["steps"] == 144 and d["steps_requested"] == 48 and d["steps_note"]
+    assert d["launches"]["count"] == 6 and d["launches"]["ms_min"] <= d["launches"]["ms_mean"] <= d["launches"]["ms_max"]
     assert d["value"] > 0 and d["higher_is_better"] is True
     assert d["config"]["workload"] and d["dtype"] == "f32" and d["scaling"] == "strong"
     rf = d["roofline"]

@@ -1,0 +1,172 @@
+"""The fp64 engine's exp, log and constant-divisor division
+(topoflow-glacier_amd/csrc/tfg_fastmath.hpp), which replace the device libm's
+exp and log and the IEEE division sequence in every fp64 step:
+
+- div_k(x, c, RN(1/c)) equals numpy's x / c bit for bit (correctly rounded),
+  over random magnitudes and random divisors, and keeps -0, +-inf and NaN;
+- exp_k is within 1 ulp of numpy's np.exp (the reference's exponential,
+  e.g. :551-556, :788-802, :919, SF:610, SF:652, :1041) over the arguments the
+  physics feeds it and over the whole finite range, and gives inf, 0 and NaN
+  where np.exp does; on the device it equals the device libm's exp bit for bit;
+- log_k is within 1 ulp of np.log (:670, :888, and em_air's 1/7 power at
+  :1167) over the physics' arguments and the whole positive range, with
+  np.log's special values.
+
+The CPU tests build the same header for the host (g++, std::fma in place of
+the device's scalar-operand FMA); the GPU test checks that the device computes
+exactly what the host build does.  The fixture tests (test_gpu_parity.py)
+check the engine as a whole against the reference at 1e-10.
+"""
+
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests.harness import ROOT
+
+SRC = ROOT / "tests" / "native" / "fastmath_host.cpp"
+HEADER = ROOT / "topoflow-glacier_amd" / "csrc" / "tfg_fastmath.hpp"
+EXP, EXP_LIBM, LOG, LOG_LIBM, DIV_61121, DIV_3600 = 3, 4, 5, 6, 7, 8
+
+# the bounds DESIGN.md section 5 states (ulps of numpy's result)
+EXP_ULPS = 1.0
+LOG_ULPS = 1.0
+
+
+@pytest.fixture(scope="module")
+def host(tmp_path_factory):
+    so = tmp_path_factory.mktemp("fastmath") / "libfastmath_host.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-shared", "-fPIC", str(SRC), "-o", str(so)],
+                   check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.fm_eval.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_int]
+    lib.fm_div.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+
+    def ev(x, which):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty_like(x)
+        lib.fm_eval(x.ctypes.data, y.ctypes.data, x.size, which)
+        return y
+
+    def div(x, c):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        c = np.ascontiguousarray(c, dtype=np.float64)
+        y = np.empty_like(x)
+        lib.fm_div(x.ctypes.data, c.ctypes.data, y.ctypes.data, x.size)
+        return y
+
+    return ev, div
+
+
+def _ulps(a, b):
+    """|a - b| in ulps of b (both finite)."""
+    return np.abs(a - b) / np.spacing(np.abs(b))
+
+
+def _wide(rng, n, lo_exp, hi_exp):
+    """Random doubles, log-uniform magnitudes 2^lo_exp .. 2^hi_exp, both signs."""
+    m = rng.uniform(1.0, 2.0, n)
+    e = rng.integers(lo_exp, hi_exp, n)
+    return np.ldexp(m, e) * rng.choice([-1.0, 1.0], n)
+
+
+def exp_arguments(rng):
+    """What the physics feeds exp: the pressure exponent (elev 0-9000 m, 200-330 K),
+    Brutsaert's 17.3 T / (T + 237.3), the albedo decay -n r, 0.0614 T_dew, the
+    clear-sky a + b m_opt, em_air's log(x) / 7; then the whole finite range."""
+    phys = np.concatenate([rng.uniform(-2.0, 0.2, 200_000), rng.uniform(-6.0, 3.5, 200_000),
+                           rng.uniform(-130.0, 0.0, 200_000), rng.uniform(-8.0, 0.5, 200_000)])
+    return phys, rng.uniform(-745.0, 709.7, 400_000)
+
+
+def log_arguments(rng):
+    """What the physics feeds log: e_air / 6.1121, max((z - h_snow) / z0, 0.01),
+    (e_air / 10) / T_air_K; then every positive normal and subnormal magnitude."""
+    phys = np.exp(rng.uniform(np.log(1e-8), np.log(1e6), 600_000))
+    near_one = 1.0 + rng.uniform(-0.3, 0.3, 200_000)
+    return np.concatenate([phys, near_one]), np.abs(_wide(rng, 400_000, -1074, 1024))
+
+
+SPECIAL = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-320, -1e-320, 5e-324, 1.0, -1.0, 1e308, -1e308,
+                    709.78, 709.79, -745.1, -745.2, 1024.5, -1075.5, 1e18, -1e18])
+
+
+def _same(a, b):
+    """Equal as values, NaN where NaN, and the same sign of zero."""
+    a, b = np.asarray(a), np.asarray(b)
+    return bool(np.all((a == b) & (np.signbit(a) == np.signbit(b)) | (np.isnan(a) & np.isnan(b))))
+
+
+def test_division_by_a_constant_is_correctly_rounded(host):
+    _, div = host
+    rng = np.random.default_rng(11)
+    x = _wide(rng, 1_000_000, -60, 60)
+    c = np.abs(_wide(rng, 1_000_000, -20, 20))
+    assert np.array_equal(div(x, c), x / c)
+    for c0 in (6.1121, 3600.0, 1000.0, 10.0, 2016.0, 0.001, 0.2617993877991494):  # the engine's divisors
+        cc = np.full_like(x, c0)
+        assert np.array_equal(div(x, cc), x / cc), c0
+    with np.errstate(invalid="ignore", divide="ignore"):
+        cc = np.full_like(SPECIAL, 6.1121)
+        assert _same(div(SPECIAL, cc), SPECIAL / cc)
+
+
+def test_exp_within_one_ulp_of_numpy(host):
+    ev, _ = host
+    rng = np.random.default_rng(12)
+    worst = {}
+    for name, x in zip(("physics", "finite range"), exp_arguments(rng)):
+        ref = np.exp(x)
+        ok = ref > 0
+        worst[name] = float(_ulps(ev(x, EXP)[ok], ref[ok]).max())
+    assert max(worst.values()) <= EXP_ULPS, worst
+    with np.errstate(over="ignore", under="ignore", invalid="ignore"):
+        assert _same(ev(SPECIAL[[2, 3, 4, 0, 1, 11, 10]], EXP), np.exp(SPECIAL[[2, 3, 4, 0, 1, 11, 10]]))
+
+
+def test_log_within_one_ulp_of_numpy(host):
+    ev, _ = host
+    rng = np.random.default_rng(13)
+    worst = {}
+    for name, x in zip(("physics", "positive range"), log_arguments(rng)):
+        ref = np.log(x)
+        ok = ref != 0
+        worst[name] = float(_ulps(ev(x, LOG)[ok], ref[ok]).max())
+        assert np.all(ev(x, LOG)[~ok] == 0.0)
+    assert max(worst.values()) <= LOG_ULPS, worst
+    with np.errstate(divide="ignore", invalid="ignore"):
+        assert _same(ev(SPECIAL, LOG), np.log(SPECIAL))
+
+
+def _device(x, which):
+    from topoflow_glacier import _native
+
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty_like(x)
+    _native.check(_native.load().tfg_selftest_powers(0, x.ctypes.data_as(ctypes.c_void_p), x.size, which,
+                                                     out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+@pytest.mark.gpu
+def test_fastmath_on_the_device(host):
+    """The device computes what the host build computes, bit for bit; its exp_k
+    equals the device libm's exp bit for bit; its log_k is within 1 ulp of the
+    device libm's log."""
+    ev, _ = host
+    rng = np.random.default_rng(14)
+    xe = np.concatenate([*exp_arguments(rng), SPECIAL])
+    assert _same(_device(xe, EXP), ev(xe, EXP))
+    assert _same(_device(xe, EXP), _device(xe, EXP_LIBM))
+    xl = np.concatenate([*log_arguments(rng), SPECIAL])
+    got = _device(xl, LOG)
+    assert _same(got, ev(xl, LOG))
+    libm = _device(xl, LOG_LIBM)
+    ok = np.isfinite(libm) & (libm != 0)
+    assert _ulps(got[ok], libm[ok]).max() <= LOG_ULPS and _same(got[~ok], libm[~ok])
+    xd = np.concatenate([_wide(rng, 400_000, -60, 60), SPECIAL])
+    for which, c in ((DIV_61121, 6.1121), (DIV_3600, 3600.0)):
+        with np.errstate(invalid="ignore"):
+            assert _same(_device(xd, which), xd / c)

@@ -554,11 +554,27 @@ __global__ void k_window_nan(const int64_t* __restrict__ tot, int64_t n, int32_t
 
 enum : uint8_t { kUnknown = 0, kOk = 1, kDirty = 2 };
 
-// tfg_selftest_powers: the fp64 engine's power rewrites (tfg_physics.hpp) on device
+// tfg_selftest_powers: the fp64 engine's power rewrites (tfg_physics.hpp) and
+// its exp / log / constant-divisor division (tfg_fastmath.hpp) on device, with
+// the device libm's exp and log beside them
 __global__ void k_selftest_powers(const double* __restrict__ x, double* __restrict__ y, int64_t n, int which) {
   const double inv7 = 1.0 / 7.0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    y[i] = which == 0 ? tfg::pow4(x[i]) : which == 1 ? tfg::pow1p5(x[i]) : tfg::pow_small_root(x[i], inv7);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    double r;
+    switch (which) {
+      case 0: r = tfg::pow4(v); break;
+      case 1: r = tfg::pow1p5(v); break;
+      case 2: r = tfg::pow_small_root(v, inv7); break;
+      case 3: r = tfg_fm::exp_k(v); break;
+      case 4: r = exp(v); break;
+      case 5: r = tfg_fm::log_k(v); break;
+      case 6: r = log(v); break;
+      case 7: r = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
+      default: r = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
+    }
+    y[i] = r;
+  }
 }
 
 struct tfg_handle {
@@ -767,6 +783,7 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.rho_air_Cp_air = q.rho_air * q.Cp_air;
   p.rho_air_Lv = q.rho_air * q.Lv;
   p.rho_H2O_Lf = q.rho_H2O * q.Lf;
+  p.inv_rho_H2O_Lf = 1.0 / p.rho_H2O_Lf;
   p.lhc = q.latent_heat_constant;
   p.sea_p0 = q.sea_level_p0;
   p.negM_g = -q.M_mass_air * q.g;
@@ -778,7 +795,6 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.kappa = q.kappa;
   p.z0 = q.z0_air;
   p.sigma = q.sigma;
-  p.em_surf = q.em_surf;
   p.em_surf_sigma = q.em_surf * q.sigma;
   p.one_minus_em_surf = 1.0 - q.em_surf;
   p.one_seventh = 1.0 / 7.0;
@@ -795,7 +811,7 @@ void derive_params(const tfg_params& q, DevParams& p) {
     const double e = (q.rho_ice * q.Cp_ice) * q.h_active_layer * (q.T0 - 0.0);
     p.Ecci0 = (e >= 0.0 || e != e) ? e : 0.0;
   }
-  p.omega = (360.0 / 24.0) * (pi / 180.0);
+  p.omega = tfg::kOmega;  // (360 / 24) * (pi / 180)
   p.half_pi = pi / 2.0;
   p.twopi = 2.0 * pi;
   p.qscale = 68719476736.0;  // 2^36
@@ -1491,7 +1507,7 @@ int tfg_reset_diag(tfg_handle* h) {
 }
 
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out) {
-  if (!x || !out || n < 0 || which < 0 || which > 2) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  if (!x || !out || n < 0 || which < 0 || which > 8) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
   if (n == 0) return TFG_OK;
   HIPCHK(nullptr, hipSetDevice(device));
   double* d = nullptr;

@@ -1,0 +1,195 @@
+// tfg_fastmath.hpp -- fp64 exp, log and division by a constant for the fp64
+// ("exact") engine.  The fp64 step is issue-bound (1450
+// VALU instructions per wave and cell-step at ~90 % of the vector pipe before
+// this file); per step it evaluates eight exp, three log and about fifteen
+// divisions by a model constant.
+//
+//   log_k(x)       fdlibm's log (k ln2 + log1p(f) with s = f/(2+f) and a
+//                  degree-14 polynomial in s), the division by a two-step
+//                  Newton reciprocal, the polynomials by FMA.  Within 1 ulp of
+//                  numpy's log (measured: tests/test_fastmath.py; 1.7 % of the
+//                  physics' arguments differ by one ulp) where the device
+//                  libm's double-double log is ~100 VALU instructions; this is
+//                  ~40.
+//   div_k(x, c, rc)  x / c for a constant c with rc = RN(1/c) known up front:
+//                  q = RN(x rc), then one FMA correction step, which gives the
+//                  correctly rounded quotient, IEEE division's result bit for
+//                  bit (Markstein's theorem; tests/test_fastmath.py checks 1e6
+//                  random pairs and the engine's divisors); 6 VALU instead of
+//                  the 11 of the general sequence (v_div_scale x2, v_rcp, five
+//                  FMAs, v_div_fmas, v_div_fixup).
+//   exp_k(x)       the device libm's exp restated operation for operation
+//                  (Cody-Waite reduction, degree-12 polynomial, ldexp, the same
+//                  overflow/underflow selects): the same results bit for bit
+//                  and the same cost, so that the host build below computes
+//                  exactly what the device does.
+//
+// Same-box A/B at 4096^2 (scripts/gpu_ab_f64.sh, profiles/r3f_ab_f64.log):
+// 26.6 -> 31.2 G cell-updates/s (+17 %).  Holding exp's polynomial
+// coefficients in SGPRs as well (the scalar operand of v_fma_f64 instead of a
+// v_mov pair feeding v_fmac_f64) saves ~60 more VALU instructions of the step
+// but raises it from 118 to 144 VGPRs (3 instead of 4 waves per SIMD): 29.5
+// (profiles/r3e_ab_f64.log); only log_k's constants are placed so.
+//
+// The same functions compile for the host (g++), with std::fma in place of the
+// scalar-operand FMA: tests/test_fastmath.py builds them and checks them
+// against numpy's exp, log and division over the physics' ranges and the
+// special values, and its GPU test checks that the device computes exactly
+// what the host build does.  Every fp64 step (grid k_fused<double>, one-cell
+// k_cell / k_cell_run / k_cell_many) calls these, so the one-cell kernels still
+// equal the grid kernel bit for bit.
+#pragma once
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TFG_FM_HD __host__ __device__
+#else
+#define TFG_FM_HD
+#endif
+#include <cmath>
+#include <cstdint>
+
+// No FMA contraction inside these functions (HIP compiles with contraction on
+// by default; the host build passes -ffp-contract=off): device and host then
+// round every operation alike.
+#if defined(__clang__)
+#define TFG_FM_NO_CONTRACT _Pragma("clang fp contract(off)")
+#else
+#define TFG_FM_NO_CONTRACT
+#endif
+
+// TFG_FM_SGPR_CONST=0 (A/B switch) leaves the placement of log_k's constants
+// to the compiler (plain FMAs; the same results; measured equal speed).
+#ifndef TFG_FM_SGPR_CONST
+#define TFG_FM_SGPR_CONST 1
+#endif
+
+namespace tfg_fm {
+
+// d = a * b + c with b (fma_vsv) or c (fma_vvs) a wave-uniform constant held in
+// an SGPR pair.  Host: std::fma.
+TFG_FM_HD inline double fma_vsv(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && TFG_FM_SGPR_CONST
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+  return d;
+#else
+  return std::fma(a, b, c);
+#endif
+}
+TFG_FM_HD inline double fma_vvs(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && TFG_FM_SGPR_CONST
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+#else
+  return std::fma(a, b, c);
+#endif
+}
+TFG_FM_HD inline double fma_vv(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_fma(a, b, c);
+#else
+  return std::fma(a, b, c);
+#endif
+}
+
+TFG_FM_HD inline double bits_to_double(uint64_t b) {
+  union { uint64_t u; double d; } v{b};
+  return v.d;
+}
+
+// ---------------------------------------------------------------------------
+// exp: the device libm's exp (ROCm 7.2 device libs) as the compiler emits it
+// for this engine (the constants below are read off its machine code).
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double exp_k(double x) {
+  TFG_FM_NO_CONTRACT
+  const double dn = std::rint(x * bits_to_double(0x3ff71547652b82feull));  // x / ln 2
+  double t = fma_vv(dn, bits_to_double(0xbfe62e42fefa39efull), x);          // - dn ln2_hi
+  t = fma_vv(dn, bits_to_double(0xbc7abc9e3b39803full), t);                 // - dn ln2_lo
+  double p = fma_vv(t, bits_to_double(0x3e5ade156a5dcb37ull), bits_to_double(0x3e928af3fca7ab0cull));
+  p = fma_vv(t, p, bits_to_double(0x3ec71dee623fde64ull));
+  p = fma_vv(t, p, bits_to_double(0x3efa01997c89e6b0ull));
+  p = fma_vv(t, p, bits_to_double(0x3f2a01a014761f6eull));
+  p = fma_vv(t, p, bits_to_double(0x3f56c16c1852b7b0ull));
+  p = fma_vv(t, p, bits_to_double(0x3f81111111122322ull));
+  p = fma_vv(t, p, bits_to_double(0x3fa55555555502a1ull));
+  p = fma_vv(t, p, bits_to_double(0x3fc5555555555511ull));
+  p = fma_vv(t, p, bits_to_double(0x3fe000000000000bull));
+  p = fma_vv(t, p, 1.0);
+  p = fma_vv(t, p, 1.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int k = (int)dn;  // v_cvt_i32_f64 saturates
+#else
+  const int k = (int)std::fmin(std::fmax(dn, -2147483648.0), 2147483647.0);
+#endif
+  double z = std::ldexp(p, k);
+  z = (x > 1024.0) ? (double)INFINITY : z;
+  z = (x < -1075.0) ? 0.0 : z;
+  return z;
+}
+
+// ---------------------------------------------------------------------------
+// log: fdlibm e_log.c's reduction and polynomial (Lg1..Lg7), one formula for
+// every argument, FMA Horner, s = f / (2 + f) by a Newton reciprocal.
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double rcp_approx(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcp(d);  // v_rcp_f64
+#else
+  return (double)(1.0f / (float)d);  // a coarser seed than the device's: two Newton steps cover both
+#endif
+}
+
+TFG_FM_HD inline double log_k(double x) {
+  TFG_FM_NO_CONTRACT
+#if defined(__HIP_DEVICE_COMPILE__)
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1) for finite nonzero x
+  int k = __builtin_amdgcn_frexp_exp(x);
+#else
+  int k = 0;
+  double m = std::frexp(x, &k);
+#endif
+  const bool lo = m < bits_to_double(0x3fe6a09e667f3bcdull);  // sqrt(1/2)
+  m = lo ? m + m : m;
+  k = lo ? k - 1 : k;
+  const double f = m - 1.0;  // [sqrt(1/2) - 1, sqrt(2) - 1), exact
+  const double d = f + 2.0;
+  double r = rcp_approx(d);
+  r = fma_vv(fma_vv(-d, r, 1.0), r, r);
+  r = fma_vv(fma_vv(-d, r, 1.0), r, r);
+  const double s = f * r;
+  const double dk = (double)k;
+  const double z = s * s, w = z * z;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+               Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  const double t1 = w * fma_vvs(w, fma_vsv(w, Lg6, Lg4), Lg2);
+  const double t2 = z * fma_vvs(w, fma_vvs(w, fma_vsv(w, Lg7, Lg5), Lg3), Lg1);
+  const double R = t2 + t1;
+  const double hfsq = 0.5 * f * f;
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double y = fma_vsv(dk, ln2_hi, -((hfsq - fma_vv(s, hfsq + R, dk * ln2_lo)) - f));
+  // special values: log(+-0) = -inf, log(x < 0) = NaN, log(+inf) = +inf; NaN propagates through the above
+  if (x == 0.0) return -(double)INFINITY;
+  if (x < 0.0) return (double)NAN;
+  if (x == (double)INFINITY) return x;
+  return y;
+}
+
+// ---------------------------------------------------------------------------
+// x / c for a constant c, rc = RN(1/c) (a literal 1.0 / c, or a reciprocal the
+// host computed in fp64): correctly rounded, like the IEEE division.  Where the
+// residual is zero (q exact, including x = +-0) or NaN (x infinite or NaN) the
+// first product is already the quotient (and keeps -0 and +-inf).
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double div_k(double x, double c, double rc) {
+  TFG_FM_NO_CONTRACT
+  const double q = x * rc;
+  const double e = fma_vv(-q, c, x);
+  const double q1 = fma_vv(e, rc, q);
+  return (e < 0.0 || e > 0.0) ? q1 : q;
+}
+
+}  // namespace tfg_fm

@@ -20,7 +20,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tfg_fastmath.hpp"
+
 namespace tfg {
+
+using tfg_fm::div_k;
+using tfg_fm::exp_k;
+using tfg_fm::log_k;
+
+// Earth_Angular_Velocity() (SF:252) [rad/h] and its correctly rounded
+// reciprocal (the divisor of the sunrise/sunset offsets, SF:783-830).
+constexpr double kOmega = (360.0 / 24.0) * (3.141592653589793 / 180.0);
+constexpr double kInvOmega = 1.0 / kOmega;
 
 // ---------------------------------------------------------------------------
 // Constants derived on the host (fp64) from tfg_params, in the reference's
@@ -37,11 +48,12 @@ struct DevParams {
   double eps, one_minus_eps;  // :817
   double gz;                  // g*z (z = 10 m)                    :640
   double z, kappa, z0;        // :670
-  double em_surf_sigma, sigma, one_minus_em_surf, em_surf;
+  double em_surf_sigma, sigma, one_minus_em_surf;
+  double inv_rho_H2O_Lf;      // RN(1/(rho_H2O*Lf)): div_k of :1368, :1428
   double one_seventh;         // np.float64(1)/7                   :292
   double T0;                  // T0_cc                             :389
   double Ecci0;               // initial ice cold content          :394-395
-  double inv_dt, inv_dt_rhoLf, inv_z0;  // reciprocals for the fast variant
+  double inv_dt, inv_dt_rhoLf, inv_z0;  // reciprocals (fast variant; inv_dt, inv_z0 also div_k's)
   double ws, wi;              // rho_H2O/rho_snow, rho_H2O/rho_ice :385-386
   double days_per_dt;         // dt/86400                          :287
   double sin_lat, cos_lat;    // of lat*(pi/180)                   SF:730-733
@@ -184,8 +196,8 @@ __device__ __forceinline__ void slope_sun_offsets(const DevParams& p, const Cell
   double arg = -1.0 * s.tan_eq * tan_d;
   arg = npmin(npmax(-1.0, arg), 1.0);
   const double ac = acos(arg);
-  const double t_sr = -1.0 * ac / p.omega;
-  const double t_ss = ac / p.omega;
+  const double t_sr = div_k(-1.0 * ac, p.omega, kInvOmega);
+  const double t_ss = div_k(ac, p.omega, kInvOmega);
   T_sr = npmax(t_sr + s.t_noon, flat_sr);
   T_ss = npmin(t_ss + s.t_noon, flat_ss);
 }
@@ -204,7 +216,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   // update_snow_meltrate :1364-1373
   double E_in = Q_sum * dt;
   double E_rem = npmax(E_in - st.Eccs, 0.0);
-  double SM = (E_rem / dt) / p.rho_H2O_Lf;
+  double SM = div_k(div_k(E_rem, dt, p.inv_dt), p.rho_H2O_Lf, p.inv_rho_H2O_Lf);
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
   SM = npmax(SM, 0.0);
@@ -213,7 +225,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   // update_swe :1594-1606
   double h_swe = st.h_swe + P_snow * dt;
   double t = npmin(SM * 3600.0, h_swe);
-  SM = t / 3600.0;
+  SM = div_k(t, 3600.0, 1.0 / 3600.0);
   h_swe = h_swe - SM * dt * 3600.0;
   h_swe = npmax(h_swe, 0.0);
   // update_snowfall_cold_content :1507-1537
@@ -225,23 +237,23 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   }
   // update_ice_meltrate :1418-1434
   E_rem = npmax(E_in - st.Ecci, 0.0);
-  double IM = (E_rem / dt) / p.rho_H2O_Lf;
+  double IM = div_k(div_k(E_rem, dt, p.inv_dt), p.rho_H2O_Lf, p.inv_rho_H2O_Lf);
   IM = npmax(IM, 0.0);
   IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
   double Ecci = npmax(st.Ecci - E_in, 0.0);
   Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;  // previous-step h_ice
   // enforce_max_ice_meltrate :1473-1480
-  IM = npmin(IM, st.h_iwe / dt);
+  IM = npmin(IM, div_k(st.h_iwe, dt, p.inv_dt));
   IM = npmax(IM, 0.0);
   // update_IM_integral :1493
   if (valid) d.IM += IM * p.da_m2 * dt * 3600.0;
   // update_iwe :1612-1617
   t = npmin(IM * 3600.0, st.h_iwe);
-  IM = t / 3600.0;
+  IM = div_k(t, 3600.0, 1.0 / 3600.0);
   double h_iwe = st.h_iwe - IM * dt * 3600.0;
   h_iwe = npmax(h_iwe, 0.0);
   // update_combined_meltrate :1441-1443
-  const double M_total = IM + SM + P_rain / 3600.0;
+  const double M_total = IM + SM + div_k(P_rain, 3600.0, 1.0 / 3600.0);
   // update_snow_depth :1711 / update_ice_depth :1726
   const double h_snow = h_swe * p.ws;
   const double h_ice = h_iwe * p.wi;
@@ -269,7 +281,7 @@ __device__ __forceinline__ double albedo_step(const DevParams& p, CellState& st,
   // n: where(tot >= .03, 0, n); where(tot < .03, n + days_per_dt, n)
   st.n = window_days(st.n, st.tot_q, p.thr_q, p.days_per_dt);
   const double r = (T_air > 0.0) ? 0.12 : 0.05;
-  const double snow_albedo = 0.4 + 0.44 * exp(-st.n * r);
+  const double snow_albedo = 0.4 + 0.44 * exp_k(-st.n * r);
   double albedo = (st.h_snow > 0.0) ? snow_albedo : st.albedo;
   if (st.h_snow == 0.0 && st.h_ice > 0.0) albedo = 0.3;
   if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
@@ -310,7 +322,7 @@ __device__ __forceinline__ double pow1p5(double x) {
 // in its chain unless SATTERLUND is set.
 __device__ __forceinline__ double pow_small_root(double x, double inv_n) {
 #pragma clang fp contract(off)
-  return exp(log(x) * inv_n);
+  return exp_k(log_k(x) * inv_n);
 }
 
 // ---------------------------------------------------------------------------
@@ -336,8 +348,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
   // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556
   const double T_K = T_air + 273.15;
-  double p0 = p.sea_p0 * exp(p.negM_g * s.elev / (p.R * T_K));
-  p0 = p0 / 1000.0;
+  double p0 = p.sea_p0 * exp_k(p.negM_g * s.elev / (p.R * T_K));
+  p0 = div_k(p0, 1000.0, 1.0 / 1000.0);
   p0 = p0 * 10.0;
   // :567, :576, :585, :604, :613, :623
   const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
@@ -351,26 +363,26 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // saturation vapour pressure (air) :788-802
   double e_sat_air;
   if (!p.satterlund) {
-    e_sat_air = 0.611 * exp((17.3 * T_air) / (T_air + 237.3));
+    e_sat_air = 0.611 * exp_k((17.3 * T_air) / (T_air + 237.3));
   } else {
-    e_sat_air = pow(opaque(10.0), 11.4 - 2353.0 / (T_air + 273.15)) / 1000.0;
+    e_sat_air = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_air + 273.15)), 1000.0, 1.0 / 1000.0);
   }
   e_sat_air = e_sat_air * 10.0;
   // :817-826
   double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
-  e = e / 1000.0;
+  e = div_k(e, 1000.0, 1.0 / 1000.0);
   const double e_air = e * 10.0;
   const double RH = e_air / e_sat_air;  // :838
   // :888-893
-  const double log_term = log(e_air / 6.1121);
+  const double log_term = log_k(div_k(e_air, 6.1121, 1.0 / 6.1121));
   const double T_dew = 257.14 * log_term / (18.678 - log_term);
   // :906-910 (previous-step depths)
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
   double e_sat_surf;
   if (!p.satterlund) {
-    e_sat_surf = 0.611 * exp((17.3 * T_surf) / (T_surf + 237.3));
+    e_sat_surf = 0.611 * exp_k((17.3 * T_surf) / (T_surf + 237.3));
   } else {
-    e_sat_surf = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15)) / 1000.0;
+    e_sat_surf = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
   }
   e_sat_surf = e_sat_surf * 10.0;
   // :640-644, per cell
@@ -379,13 +391,13 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (bot == 0.0) bot = 0.01;
   const double Ri = top / bot;
   // :670-726
-  const double arg = p.kappa / log(npmax((p.z - h_snow) / p.z0, 0.01));
+  const double arg = p.kappa / log_k(npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01));
   const double Dn = uz * (arg * arg);
   const double Dh = (Ri > 0.0) ? Dn / (1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
   // :744-745
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
   // :919-920
-  const double W_p = 1.12 * exp(0.0614 * T_dew);
+  const double W_p = 1.12 * exp_k(0.0614 * T_dew);
   // :853 (SURFACE uses the air RH)
   const double e_surf = RH * e_sat_surf;
   // :931-934
@@ -398,12 +410,12 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
-  const double tau = npmin(npmax(exp(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
+  const double tau = npmin(npmax(exp_k(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
   double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos(u.omega_th + s.dlon) + s.sin_leq * u.sin_d);
   K_ET = npmax(K_ET, 0.0);
   const double a_s = -0.0363 - (0.0084 * W_p);
   const double b_s = -0.0572 - (0.0173 * W_p);
-  const double gam_s = (1.0 - exp(a_s + (b_s * u.m_opt))) + p2.dust;
+  const double gam_s = (1.0 - exp_k(a_s + (b_s * u.m_opt))) + p2.dust;
   const double K_dif = 0.5 * gam_s * u.k_et_flat;
   const double K_global = tau * u.k_et_flat + K_dif;
   const double K_bs = 0.5 * gam_s * albedo * K_global;
@@ -417,10 +429,10 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * pow_small_root((e_air / 10.0) / T_air_K, p3.one_seventh);
+    const double term1 = p3.one_minus_F_172 * pow_small_root(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K, p3.one_seventh);
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
-    em_air = 1.08 * (1.0 - exp(-1.0 * pow(e_air, T_air_K / 2016.0)));
+    em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
@@ -506,7 +518,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   d.PS += P_snow * p.da_m2 * dt;
   // :817-826
   double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
-  e = e / 1000.0;
+  e = div_k(e, 1000.0, 1.0 / 1000.0);
   const double e_air = e * 10.0;
   const double T_air_K = T_air + 273.15;
   // window and days since snowfall (:1023-1040), ahead of the albedo exp
@@ -521,16 +533,17 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const double x_p0 = p.negM_g * s.elev / (p.R * T_K);        // :551
     const double x_es = (17.3 * T_air) / (T_air + 237.3);        // :788
     const double x_alb = -st.n * r_alb;                          // :1041
-    ex1 = exp(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
+    ex1 = exp_k(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
   if (X.mine(X_LOG1))  // :670, :888, and em_air's root (:1167, pow_small_root)
-    lg1 = log(lane == 1 ? npmax((p.z - h_snow) / p.z0, 0.01) : (lane == 2 ? (e_air / 10.0) / T_air_K : e_air / 6.1121));
+    lg1 = log_k(lane == 1 ? npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01)
+                          : (lane == 2 ? div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K : div_k(e_air, 6.1121, 1.0 / 6.1121)));
   if (X.mine(X_TRIG1)) {
     cos_wl = cos(u.omega_th + s.dlon);                                        // SF:867 (one argument)
     ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));            // SF:325 (one argument)
   }
   if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
-    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : T_air_K / 2016.0);
+    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : div_k(T_air_K, 2016.0, 1.0 / 2016.0));
   X.put(X_EXP1, ex1);
   X.put(X_LOG1, lg1);
   X.put(X_TRIG1, lane == 1 ? ac : cos_wl);
@@ -547,10 +560,10 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
 
   // :551-556
   double p0 = p.sea_p0 * e_p0;
-  p0 = p0 / 1000.0;
+  p0 = div_k(p0, 1000.0, 1.0 / 1000.0);
   p0 = p0 * 10.0;
   // :788-802, :838
-  double e_sat_air = !p.satterlund ? 0.611 * e_es : pw_es / 1000.0;
+  double e_sat_air = !p.satterlund ? 0.611 * e_es : div_k(pw_es, 1000.0, 1.0 / 1000.0);
   e_sat_air = e_sat_air * 10.0;
   const double RH = e_air / e_sat_air;
   // :888-893, :906-910
@@ -572,8 +585,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
   st.albedo = albedo;
   // sunrise / sunset on the slope (SF:783-830)
-  const double T_sr = npmax(-1.0 * ac / p.omega + s.t_noon, u.flat_sr);
-  const double T_ss = npmin(ac / p.omega + s.t_noon, u.flat_ss);
+  const double T_sr = npmax(div_k(-1.0 * ac, p.omega, kInvOmega) + s.t_noon, u.flat_sr);
+  const double T_ss = npmin(div_k(ac, p.omega, kInvOmega) + s.t_noon, u.flat_ss);
   const double T_surf_K = T_surf + 273.15;
 
   // ---- level 2: after T_dew, T_surf and RH
@@ -582,7 +595,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
     if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
     if (lane == 3) ea2 = log_em * p.one_seventh;                                    // :1167 (pow_small_root)
-    ex2 = exp(ea2);
+    ex2 = exp_k(ea2);
   }
   if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15));  // :796 (surface)
   if (X.mine(X_ATAN2) && P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
@@ -592,7 +605,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   X.put(X_POW2, pw2);
   X.put(X_ATAN2, at2);
   if (W > 1) lds_level_barrier();
-  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : X.get(X_POW2, pw2, 0) / 1000.0;
+  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : div_k(X.get(X_POW2, pw2, 0), 1000.0, 1.0 / 1000.0);
   e_sat_surf = e_sat_surf * 10.0;
   const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
@@ -605,7 +618,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
 
   // ---- level 3: after W_p
   double ex3 = 0.0;
-  if (X.mine(X_EXP3)) ex3 = exp(lane == 1 ? a_s + (b_s * u.m_opt) : a_sa + (b_sa * u.m_opt));  // SF:610, SF:652
+  if (X.mine(X_EXP3)) ex3 = exp_k(lane == 1 ? a_s + (b_s * u.m_opt) : a_sa + (b_sa * u.m_opt));  // SF:610, SF:652
   X.put(X_EXP3, ex3);
   if (W > 1) lds_level_barrier();
   const double tau = npmin(npmax(X.get(X_EXP3, ex3, 0) - p.dust, 0.0), 1.0);
