@@ -76,7 +76,7 @@ __device__ __forceinline__ void load_one_cell(const DevParams& p, int64_t np, co
     cs.h_ice = cs.h_iwe * p.wi;   // :1726
   }
   cs.tot_q = tot[0];
-  sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np]};
+  sx = {geo[0], geo[np], geo[2 * np], geo[3 * np], geo[4 * np], geo[5 * np], geo[6 * np]};
 }
 
 // Write the state back and add the step(s)' diagnostics to the slab row `srow`
@@ -330,9 +330,9 @@ __global__ void k_prepare_geo(const DevParams p, const R* __restrict__ stat, flo
   }
 }
 
-// Exact engine: CellStatic planes [6][n_pad] fp64 (elev, cos_leq, sin_leq,
-// dlon, tan_eq, t_noon), derived once per static-raster change instead of
-// once per launch.
+// Exact engine: CellStatic planes [kStaticPlanes][n_pad] fp64 (elev, cos_leq,
+// sin_leq, dlon, tan_eq, cos_dlon, sin_dlon), derived once per static-raster
+// change instead of once per launch.
 template <class R>
 __global__ void k_prepare_static(const DevParams p, const R* __restrict__ stat, double* __restrict__ gx, int64_t n_pad) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
@@ -342,7 +342,8 @@ __global__ void k_prepare_static(const DevParams p, const R* __restrict__ stat, 
     gx[2 * n_pad + i] = s.sin_leq;
     gx[3 * n_pad + i] = s.dlon;
     gx[4 * n_pad + i] = s.tan_eq;
-    gx[5 * n_pad + i] = s.t_noon;
+    gx[5 * n_pad + i] = s.cos_dlon;
+    gx[6 * n_pad + i] = s.sin_dlon;
   }
 }
 
@@ -571,6 +572,7 @@ __global__ void k_selftest_powers(const double* __restrict__ x, double* __restri
       case 5: r = tfg_fm::log_k(v); break;
       case 6: r = log(v); break;
       case 7: r = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
+      case 9: r = tfg_fm::exp_ks(v); break;
       default: r = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
     }
     y[i] = r;
@@ -1046,7 +1048,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {&h->forc, (size_t)n_frames * kNumForc * np * rs},
       {&h->stat, 3 * (size_t)np * rs},
       {&h->lwsw, 2 * (size_t)np * rs},
-      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (tfg::kGeoF * 4 + 2 * 8) : (size_t)np * 6 * 8},
+      {(void**)&h->geo, engine == TFG_F32 ? (size_t)np * (tfg::kGeoF * 4 + 2 * 8) : (size_t)np * tfg::kStaticPlanes * 8},
       {(void**)&h->st, (size_t)kNumState * np * 8},
       {(void**)&h->tot, (size_t)np * 8},
       {(void**)&h->ring, (size_t)p->ring_len * np * 4},
@@ -1507,7 +1509,7 @@ int tfg_reset_diag(tfg_handle* h) {
 }
 
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out) {
-  if (!x || !out || n < 0 || which < 0 || which > 8) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  if (!x || !out || n < 0 || which < 0 || which > 9) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
   if (n == 0) return TFG_OK;
   HIPCHK(nullptr, hipSetDevice(device));
   double* d = nullptr;

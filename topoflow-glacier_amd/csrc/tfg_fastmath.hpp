@@ -26,10 +26,13 @@
 //
 // Same-box A/B at 4096^2 (scripts/gpu_ab_f64.sh, profiles/r3f_ab_f64.log):
 // 26.6 -> 31.2 G cell-updates/s (+17 %).  Holding exp's polynomial
-// coefficients in SGPRs as well (the scalar operand of v_fma_f64 instead of a
-// v_mov pair feeding v_fmac_f64) saves ~60 more VALU instructions of the step
-// but raises it from 118 to 144 VGPRs (3 instead of 4 waves per SIMD): 29.5
-// (profiles/r3e_ab_f64.log); only log_k's constants are placed so.
+// coefficients in SGPRs at every call site (the scalar operand of v_fma_f64
+// instead of a v_mov pair feeding v_fmac_f64) saves ~60 more VALU instructions
+// of the step but raises it from 118 to 144 VGPRs (3 instead of 4 waves per
+// SIMD): 29.5 (profiles/r3e_ab_f64.log).  So exp_ks (SGPR constants) is used
+// only at the call sites that leave the step's VGPR count alone (em_air's
+// root, both saturation pressures), exp_k elsewhere; log_k's constants are
+// always scalar operands.
 //
 // The same functions compile for the host (g++), with std::fma in place of the
 // scalar-operand FMA: tests/test_fastmath.py builds them and checks them
@@ -103,20 +106,35 @@ TFG_FM_HD inline double bits_to_double(uint64_t b) {
 // exp: the device libm's exp (ROCm 7.2 device libs) as the compiler emits it
 // for this engine (the constants below are read off its machine code).
 // ---------------------------------------------------------------------------
-TFG_FM_HD inline double exp_k(double x) {
+// SGPR = true: the polynomial coefficients and reduction constants as the
+// scalar operand of v_fma_f64 (SALU moves beside the vector pipe, ~10 fewer
+// VALU instructions), where the call site's register pressure allows it
+// (exp_ks; the others exp_k): the same results either way.
+template <bool SGPR>
+TFG_FM_HD inline double fk(double a, double b, double c) {  // b constant
+  if constexpr (SGPR) return fma_vsv(a, b, c);
+  else return fma_vv(a, b, c);
+}
+template <bool SGPR>
+TFG_FM_HD inline double fp(double a, double b, double c) {  // c constant
+  if constexpr (SGPR) return fma_vvs(a, b, c);
+  else return fma_vv(a, b, c);
+}
+template <bool SGPR>
+TFG_FM_HD inline double exp_impl(double x) {
   TFG_FM_NO_CONTRACT
   const double dn = std::rint(x * bits_to_double(0x3ff71547652b82feull));  // x / ln 2
-  double t = fma_vv(dn, bits_to_double(0xbfe62e42fefa39efull), x);          // - dn ln2_hi
-  t = fma_vv(dn, bits_to_double(0xbc7abc9e3b39803full), t);                 // - dn ln2_lo
-  double p = fma_vv(t, bits_to_double(0x3e5ade156a5dcb37ull), bits_to_double(0x3e928af3fca7ab0cull));
-  p = fma_vv(t, p, bits_to_double(0x3ec71dee623fde64ull));
-  p = fma_vv(t, p, bits_to_double(0x3efa01997c89e6b0ull));
-  p = fma_vv(t, p, bits_to_double(0x3f2a01a014761f6eull));
-  p = fma_vv(t, p, bits_to_double(0x3f56c16c1852b7b0ull));
-  p = fma_vv(t, p, bits_to_double(0x3f81111111122322ull));
-  p = fma_vv(t, p, bits_to_double(0x3fa55555555502a1ull));
-  p = fma_vv(t, p, bits_to_double(0x3fc5555555555511ull));
-  p = fma_vv(t, p, bits_to_double(0x3fe000000000000bull));
+  double t = fk<SGPR>(dn, bits_to_double(0xbfe62e42fefa39efull), x);              // - dn ln2_hi
+  t = fk<SGPR>(dn, bits_to_double(0xbc7abc9e3b39803full), t);                     // - dn ln2_lo
+  double p = fp<SGPR>(t, bits_to_double(0x3e5ade156a5dcb37ull), bits_to_double(0x3e928af3fca7ab0cull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3ec71dee623fde64ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3efa01997c89e6b0ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3f2a01a014761f6eull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3f56c16c1852b7b0ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3f81111111122322ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3fa55555555502a1ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3fc5555555555511ull));
+  p = fp<SGPR>(t, p, bits_to_double(0x3fe000000000000bull));
   p = fma_vv(t, p, 1.0);
   p = fma_vv(t, p, 1.0);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -129,6 +147,8 @@ TFG_FM_HD inline double exp_k(double x) {
   z = (x < -1075.0) ? 0.0 : z;
   return z;
 }
+TFG_FM_HD inline double exp_k(double x) { return exp_impl<false>(x); }
+TFG_FM_HD inline double exp_ks(double x) { return exp_impl<TFG_FM_SGPR_CONST != 0>(x); }
 
 // ---------------------------------------------------------------------------
 // log: fdlibm e_log.c's reduction and polynomial (Lg1..Lg7), one formula for

@@ -261,11 +261,11 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       tfg::CellStaticF SF[EXACT ? 1 : C];
       if constexpr (EXACT) {
         const double* gx = reinterpret_cast<const double*>(geo);
-        double v[6][C];
+        double v[tfg::kStaticPlanes][C];
 #pragma unroll
-        for (int f = 0; f < 6; ++f) dload<C>(gx + f * n_pad, lc, v[f]);
+        for (int f = 0; f < tfg::kStaticPlanes; ++f) dload<C>(gx + f * n_pad, lc, v[f]);
 #pragma unroll
-        for (int j = 0; j < C; ++j) SX[j] = {v[0][j], v[1][j], v[2][j], v[3][j], v[4][j], v[5][j]};
+        for (int j = 0; j < C; ++j) SX[j] = {v[0][j], v[1][j], v[2][j], v[3][j], v[4][j], v[5][j], v[6][j]};
       } else {
         float gv[tfg::kGeoF][C];
 #pragma unroll

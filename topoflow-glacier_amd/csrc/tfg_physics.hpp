@@ -26,6 +26,7 @@ namespace tfg {
 
 using tfg_fm::div_k;
 using tfg_fm::exp_k;
+using tfg_fm::exp_ks;
 using tfg_fm::log_k;
 
 // Earth_Angular_Velocity() (SF:252) [rad/h] and its correctly rounded
@@ -89,8 +90,13 @@ struct CellStatic {
   double cos_leq, sin_leq;  // of lat_eq [rad]                      SF:866-868
   double dlon;              // Longitude_Offset [rad]                SF:864
   double tan_eq;            // tan(eq_lat_deg*(pi/180))             SF:325
-  double t_noon;            // Noon_Offset_Slope [h]                 SF:776
+  double cos_dlon, sin_dlon;  // of dlon: cos(omega*th + dlon) by the angle-sum identity
 };
+constexpr int kStaticPlanes = 7;  // k_prepare_static's fp64 planes, in CellStatic order
+
+// Noon_Offset_Slope (SF:776) [h], in the reference's operation order; needed
+// only where the dark test falls back to the reference's form.
+__device__ __forceinline__ double noon_offset(const DevParams& p, double dlon) { return -1.0 * dlon / p.omega; }
 
 // Per-cell model state carried between steps (fp64).
 struct CellState {
@@ -179,7 +185,8 @@ __device__ inline CellStatic derive_static(const DevParams& p, double elev, doub
   const double u3 = sb * p.sin_lat * ca;
   const double dlon = atan(u1 / (u2 - u3));
   s.dlon = dlon;
-  s.t_noon = -1.0 * dlon / p.omega;  // SF:776
+  s.cos_dlon = cos(dlon);
+  s.sin_dlon = sin(dlon);
   s.cos_leq = cos(lat_eq);
   s.sin_leq = sin(lat_eq);
   // Sunrise_Offset(eq_lat_deg, ...) SF:320-325: degrees and back
@@ -198,8 +205,41 @@ __device__ __forceinline__ void slope_sun_offsets(const DevParams& p, const Cell
   const double ac = acos(arg);
   const double t_sr = div_k(-1.0 * ac, p.omega, kInvOmega);
   const double t_ss = div_k(ac, p.omega, kInvOmega);
-  T_sr = npmax(t_sr + s.t_noon, flat_sr);
-  T_ss = npmin(t_ss + s.t_noon, flat_ss);
+  const double t_noon = noon_offset(p, s.dlon);
+  T_sr = npmax(t_sr + t_noon, flat_sr);
+  T_ss = npmin(t_ss + t_noon, flat_ss);
+}
+
+// cos(omega*th + dlon) (SF:867) from the step's cos/sin(omega*th) and the
+// cell's cos/sin(dlon): absolute error ~4e-16 against the reference's
+// cos of the rounded sum, one multiply and one multiply-subtract instead of a
+// libm cos.
+__device__ __forceinline__ double cos_hour_angle(const CellStatic& s, const tfg_uniforms& u) {
+#pragma clang fp contract(off)
+  return u.cos_wth * s.cos_dlon - u.sin_wth * s.sin_dlon;
+}
+
+// The dark test of Clear_Sky_Radiation (SF:939-941): th <= T_sr or th >= T_ss
+// with T_sr = max(-ac/omega + t_noon, flat_sr), T_ss = min(ac/omega + t_noon,
+// flat_ss), ac = acos(clip(-tan(lat_eq) tan(d))), t_noon = -dlon/omega.  With
+// x = omega*th + dlon = omega*(th - t_noon):
+//   dark  <=>  flat_dark  or  |x| >= ac  <=>  flat_dark or |x| > pi or cos(x) <= cos(ac) = arg,
+// flat_dark (th <= flat_sr or th >= flat_ss) being decided on the host.  The
+// reference's own rounding moves the boundary by < 1e-15 in cos(x) (and |x|),
+// so outside a 1e-12 margin the cosine form decides as the reference does;
+// inside it (a cell-step within ~1e-12 of sunrise or sunset on its slope) the
+// reference's form runs: acos and the offsets, as slope_sun_offsets.
+__device__ __forceinline__ bool sun_down(const DevParams& p, const CellStatic& s, const tfg_uniforms& u,
+                                         double cos_wl) {
+#pragma clang fp contract(off)
+  if (u.flat_dark) return true;
+  const double arg = npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0);
+  const double dv = cos_wl - arg;
+  const double dpi = fabs(u.omega_th + s.dlon) - 3.141592653589793;
+  if (fabs(dv) > 1e-12 && fabs(dpi) > 1e-12) return dpi > 0.0 || dv < 0.0;
+  double T_sr, T_ss;
+  slope_sun_offsets(p, s, u.tan_d, u.flat_sr, u.flat_ss, T_sr, T_ss);
+  return (u.th <= T_sr) || (u.th >= T_ss);
 }
 
 // ---------------------------------------------------------------------------
@@ -322,7 +362,7 @@ __device__ __forceinline__ double pow1p5(double x) {
 // in its chain unless SATTERLUND is set.
 __device__ __forceinline__ double pow_small_root(double x, double inv_n) {
 #pragma clang fp contract(off)
-  return exp_k(log_k(x) * inv_n);
+  return exp_ks(log_k(x) * inv_n);
 }
 
 // ---------------------------------------------------------------------------
@@ -363,7 +403,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // saturation vapour pressure (air) :788-802
   double e_sat_air;
   if (!p.satterlund) {
-    e_sat_air = 0.611 * exp_k((17.3 * T_air) / (T_air + 237.3));
+    e_sat_air = 0.611 * exp_ks((17.3 * T_air) / (T_air + 237.3));
   } else {
     e_sat_air = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_air + 273.15)), 1000.0, 1.0 / 1000.0);
   }
@@ -380,7 +420,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
   double e_sat_surf;
   if (!p.satterlund) {
-    e_sat_surf = 0.611 * exp_k((17.3 * T_surf) / (T_surf + 237.3));
+    e_sat_surf = 0.611 * exp_ks((17.3 * T_surf) / (T_surf + 237.3));
   } else {
     e_sat_surf = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
   }
@@ -411,7 +451,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
   const double tau = npmin(npmax(exp_k(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
-  double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos(u.omega_th + s.dlon) + s.sin_leq * u.sin_d);
+  const double cos_wl = cos_hour_angle(s, u);  // SF:867
+  double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos_wl + s.sin_leq * u.sin_d);
   K_ET = npmax(K_ET, 0.0);
   const double a_s = -0.0363 - (0.0084 * W_p);
   const double b_s = -0.0572 - (0.0173 * W_p);
@@ -420,9 +461,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double K_global = tau * u.k_et_flat + K_dif;
   const double K_bs = 0.5 * gam_s * albedo * K_global;
   double K_cs = (tau * K_ET) + K_dif + K_bs;
-  double T_sr, T_ss;
-  slope_sun_offsets(p2, s, u.tan_d, u.flat_sr, u.flat_ss, T_sr, T_ss);
-  if ((u.th <= T_sr) || (u.th >= T_ss)) K_cs = 0.0;
+  if (sun_down(p2, s, u, cos_wl)) K_cs = 0.0;
   const double Qn_SW = K_cs * (1.0 - albedo);  // :1139
   const DevParams& p3 = params();  // long-wave and net flux phase
   // update_em_air :1167-1192
@@ -432,7 +471,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     const double term1 = p3.one_minus_F_172 * pow_small_root(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K, p3.one_seventh);
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
-    em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
+    em_air = 1.08 * (1.0 - exp_ks(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
@@ -538,25 +577,20 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (X.mine(X_LOG1))  // :670, :888, and em_air's root (:1167, pow_small_root)
     lg1 = log_k(lane == 1 ? npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01)
                           : (lane == 2 ? div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K : div_k(e_air, 6.1121, 1.0 / 6.1121)));
-  if (X.mine(X_TRIG1)) {
-    cos_wl = cos(u.omega_th + s.dlon);                                        // SF:867 (one argument)
-    ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));            // SF:325 (one argument)
-  }
+  if (X.mine(X_TRIG1)) ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325 (one argument)
+  cos_wl = cos_hour_angle(s, u);                                                          // SF:867
   if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
     pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : div_k(T_air_K, 2016.0, 1.0 / 2016.0));
   X.put(X_EXP1, ex1);
   X.put(X_LOG1, lg1);
-  X.put(X_TRIG1, lane == 1 ? ac : cos_wl);
+  X.put(X_TRIG1, ac);
   X.put(X_POW1, pw1);
   if (W > 1) lds_level_barrier();
   const double e_p0 = X.get(X_EXP1, ex1, 0), e_es = X.get(X_EXP1, ex1, 1), e_alb = X.get(X_EXP1, ex1, 2);
   const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1), log_em = X.get(X_LOG1, lg1, 2);
   const double pw_em = X.get(X_POW1, pw1, 0), pw_es = X.get(X_POW1, pw1, 2);
   const double pw_ta4 = pow4(T_air_K);  // :1231
-  if (W > 1) {
-    cos_wl = X.get(X_TRIG1, 0.0, 0);
-    ac = X.get(X_TRIG1, 0.0, 1);
-  }
+  if (W > 1) ac = X.get(X_TRIG1, 0.0, 0);
 
   // :551-556
   double p0 = p.sea_p0 * e_p0;
@@ -585,8 +619,9 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (st.h_snow == 0.0 && st.h_ice == 0.0) albedo = 0.15;
   st.albedo = albedo;
   // sunrise / sunset on the slope (SF:783-830)
-  const double T_sr = npmax(div_k(-1.0 * ac, p.omega, kInvOmega) + s.t_noon, u.flat_sr);
-  const double T_ss = npmin(div_k(ac, p.omega, kInvOmega) + s.t_noon, u.flat_ss);
+  const double t_noon = noon_offset(p, s.dlon);  // SF:776
+  const double T_sr = npmax(div_k(-1.0 * ac, p.omega, kInvOmega) + t_noon, u.flat_sr);
+  const double T_ss = npmin(div_k(ac, p.omega, kInvOmega) + t_noon, u.flat_ss);
   const double T_surf_K = T_surf + 273.15;
 
   // ---- level 2: after T_dew, T_surf and RH
