@@ -219,6 +219,40 @@ def test_fp64_synthetic_vs_oracle():
     assert rep["max_rel"] <= 1e-10, rep["summary"]
 
 
+@pytest.mark.parametrize("dt,nsteps", [(1.0, 72), (0.25, 192)])
+def test_fp64_dark_test_on_every_slope_through_whole_days(dt, nsteps):
+    """The fp64 engine decides day and night on each slope without acos
+    (tfg_physics.hpp sun_down: cos(omega*th + dlon) <= -tan(lat_eq) tan(d),
+    the reference's Sunrise/Sunset_Offset_Slope form inside a 1e-12 margin),
+    and takes cos(omega*th + dlon) by the angle-sum identity.  Against the
+    oracle's acos form (SF:783-830, :939-941) on 4096 cells of random slope
+    and aspect (all four sides of the compass, up to 80 degrees) through whole
+    days: outputs within 1e-10, and the cold contents, which integrate Q_sum
+    whether or not anything melts, within 1e-9.  A flipped dark decision moves
+    K_cs by the diffuse terms (tens of W m-2) and would show at ~1e-3."""
+    rng = np.random.default_rng(21)
+    ny, nx = 32, 128
+    n = ny * nx
+    cfg = dict(BASE_CFG, dt=dt)
+    static = {"elev": rng.uniform(1500.0, 3500.0, n), "slope": np.tan(np.radians(rng.uniform(0.0, 80.0, n))),
+              "aspect": rng.uniform(0.0, 360.0, n), "h0_snow": rng.uniform(0.2, 2.0, n), "h0_ice": rng.uniform(0.0, 30.0, n)}
+    static["h0_swe"] = static["h0_snow"] * 0.3
+    static["h0_iwe"] = static["h0_ice"] * 0.917
+    k = np.arange(nsteps)[:, None]
+    forcing = {"P": np.zeros((nsteps, n)),
+               "T_air": -8.0 + 4.0 * np.sin(2 * np.pi * k * dt / 24.0) + rng.uniform(-1.0, 1.0, (nsteps, n)),
+               "Hum_sp": rng.uniform(0.001, 0.004, (nsteps, n)), "P_air": rng.uniform(70000.0, 85000.0, (nsteps, n)),
+               "uz": rng.uniform(0.5, 6.0, (nsteps, n))}
+    outs, state, _ = gpu_run_fields(cfg, static, forcing, ny, nx, "float64", nsteps, fuse_steps=48)
+    ref, m = oracle_run(cfg, static, forcing)
+    for v in HIST:
+        assert parity(outs[v], ref[v], 1e-10)[0] <= 1e-10, v
+    for v in ("Eccs", "Ecci"):
+        r = np.asarray(getattr(m, v), dtype=np.float64).reshape(-1)
+        assert _rel(state[v], r) <= 1e-9, (v, _rel(state[v], r))
+    assert np.count_nonzero(np.asarray(m.Eccs)) > n // 2  # the cold contents carry the energy balance
+
+
 @pytest.mark.parametrize("engine,tol", [("float32", None), ("float64", 1e-10)])
 def test_quarter_hour_steps_vs_oracle(engine, tol):
     """BASELINE config 5's time step: dt = 0.25 h, a 288-slot snowfall window,
