@@ -38,6 +38,24 @@ def test_clock_matches_reference(name):
     assert np.array_equal(tsn, g["internal"]["TSN_offset"][:, 0])  # bit-exact
 
 
+@pytest.mark.parametrize("zone", ["America/Los_Angeles", "America/Phoenix", "America/Anchorage", "America/New_York",
+                                  "Pacific/Honolulu", "America/Boise"])
+def test_vectorised_calendar_equals_the_loop(zone):
+    """StepClock._calendar (numpy datetime64, one zone lookup per UTC day) equals
+    the per-step datetime loop (_calendar_loop, the reference's arithmetic of
+    update_julian_day :957-1004) bit for bit: starts just before DST changes
+    and the year end, a leap day, steps of 1/8 h to a day, blocks deep into a
+    run; a step the float product cannot hit exactly takes the loop."""
+    from topoflow_glacier.physics.clock import StepClock
+
+    for start in ("2013032000", "2013110100", "2014030800", "2013123100", "2016022812", "2015103118"):
+        for dt in (1.0, 0.25, 0.125, 3.0, 24.0, 0.1):
+            c = StepClock(start, dt, 46.8, -121.8, zone)
+            for k0, n in ((0, 512), (3000, 700), (8760, 512)):
+                for a, b in zip(c._calendar(k0, n), c._calendar_loop(k0, n)):
+                    assert np.array_equal(a, b), (start, dt, k0)
+
+
 @pytest.mark.parametrize("lat,lon,zone", [
     (34.0, -103.08, "America/Denver"), (34.0, -103.06, None),    # New Mexico / the Texas strip (103.064 W)
     (43.5, -116.95, "America/Boise"), (44.5, -116.75, "America/Boise"),

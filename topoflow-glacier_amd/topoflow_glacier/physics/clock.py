@@ -126,7 +126,8 @@ def _equation_of_time_hours(JD: np.ndarray, years: np.ndarray) -> np.ndarray:
     eps = np.float64(23.4397) * (np.pi / np.float64(180))
     dpy = np.float64(365.2425)
     twopi = np.float64(2) * np.pi
-    Tp = np.array([_perihelion_jd(int(y)) for y in years])
+    uy, inv = np.unique(years, return_inverse=True)
+    Tp = np.array([_perihelion_jd(int(y)) for y in uy])[inv]
     M = (twopi / dpy) * (JD - Tp)
     M = (M + twopi) % twopi
     VE = np.float64(79.3125) + dpy * (years.astype(np.float64) - np.float64(2000))
@@ -169,6 +170,53 @@ class StepClock:
         return self._calendar(k0, n)
 
     def _calendar(self, k0: int, n: int):
+        """Vectorised where the step is a whole number of seconds that the
+        float product dt*(k+1) hits exactly (dt a multiple of 1/1024 h, e.g.
+        1 h or 0.25 h): the same values as the per-step datetime loop
+        (_calendar_loop, the reference's own arithmetic), bit for bit
+        (tests/test_host.py::test_vectorised_calendar_equals_the_loop)."""
+        step_s = self.dt * 3600.0
+        if not (n > 0 and step_s == int(step_s) and self.dt * 1024.0 == int(self.dt * 1024.0)
+                and (k0 + n) * self.dt < 2.0 ** 40):
+            return self._calendar_loop(k0, n)
+        secs = (np.arange(k0 + 1, k0 + n + 1, dtype=np.int64) * int(step_s)).astype("timedelta64[s]")
+        t = np.datetime64(self.start, "s") + secs  # naive, read as UTC as the loop does
+        day = t.astype("datetime64[D]")
+        yr = t.astype("datetime64[Y]").astype(np.int64) + 1970
+        yday0 = (day - t.astype("datetime64[Y]").astype("datetime64[D]")).astype(np.int64)  # tm_yday - 1
+        sod = (t - day).astype(np.int64)
+        hour, minute, second = sod // 3600, (sod % 3600) // 60, sod % 60
+        # J = tm_yday - 1 + hour/24 + minute/1440 + second/86400, left to right (:985-990)
+        jd = ((yday0.astype(np.float64) + hour / 24) + minute / 1440) + second / 86400
+        clock_hour = (jd - np.trunc(jd)) * np.float64(24)
+        gmt = self._utc_offsets(t, day)
+        LC = ((gmt * np.float64(15)) - self.lon) / np.float64(15)  # SF:1466-1468
+        solar_noon = np.float64(12) + LC + _equation_of_time_hours(jd, yr)  # SF:1471
+        return jd, yr, gmt, clock_hour - solar_noon
+
+    def _utc_offsets(self, t: np.ndarray, day: np.ndarray) -> np.ndarray:
+        """UTC offset [h] of the zone at each UTC instant t (SF:1616-1637's
+        zoneinfo lookup): looked up once per UTC day where the offset is the
+        same at the day's first and last second, per step on a day with a
+        transition."""
+        utc = ZoneInfo("UTC")
+
+        def off(dt64) -> float:
+            d = dt64.astype("datetime64[s]").astype(datetime).replace(tzinfo=utc)
+            return d.astimezone(self.tz).utcoffset().total_seconds() / 3600.0
+
+        gmt = np.empty(len(t))
+        days, inv = np.unique(day, return_inverse=True)
+        for j, d in enumerate(days):
+            a, b = off(d), off(d + np.timedelta64(86399, "s"))
+            sel = inv == j
+            if a == b:
+                gmt[sel] = a
+            else:
+                gmt[sel] = [off(x) for x in t[sel]]
+        return gmt
+
+    def _calendar_loop(self, k0: int, n: int):
         jd = np.empty(n)
         yr = np.empty(n, dtype=np.int64)
         gmt = np.empty(n)
