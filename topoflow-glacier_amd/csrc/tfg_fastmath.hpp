@@ -32,7 +32,11 @@
 // SIMD): 29.5 (profiles/r3e_ab_f64.log).  So exp_ks (SGPR constants) is used
 // only at the call sites that leave the step's VGPR count alone (em_air's
 // root, both saturation pressures), exp_k elsewhere; log_k's constants are
-// always scalar operands.
+// always scalar operands.  A table-driven exp (2^(j/64) from LDS or from a
+// 1 KB global table, degree-5 expm1; within 1 ulp of numpy's) was measured and
+// dropped: it raised the step to 152 VGPRs and its static VALU count
+// (2430 -> 2450), and a global table load shares vmcnt with the step's forcing
+// prefetch, so waiting for it waits for the prefetch too.
 //
 // The same functions compile for the host (g++), with std::fma in place of the
 // scalar-operand FMA: tests/test_fastmath.py builds them and checks them
@@ -61,8 +65,9 @@
 #define TFG_FM_NO_CONTRACT
 #endif
 
-// TFG_FM_SGPR_CONST=0 (A/B switch) leaves the placement of log_k's constants
-// to the compiler (plain FMAs; the same results; measured equal speed).
+// TFG_FM_SGPR_CONST=0 (A/B switch) leaves the placement of the constants of
+// log_k and exp_ks to the compiler (plain FMAs, the same results; for log_k
+// alone measured equal speed, profiles/r3f_ab_f64.log).
 #ifndef TFG_FM_SGPR_CONST
 #define TFG_FM_SGPR_CONST 1
 #endif
