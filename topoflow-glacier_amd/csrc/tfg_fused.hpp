@@ -201,6 +201,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
   }
 }
 
+#ifndef TFG_WG_PERM
+#define TFG_WG_PERM 0
+#endif
 #ifndef TFG_MIN_WAVES
 #define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
 #endif
@@ -234,8 +237,14 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
   const int64_t nchunks = (ngroups + kBlock - 1) / kBlock;
-  const int64_t g0 = ((int64_t)blockIdx.x * nchunks / gridDim.x) * kBlock;
-  const int64_t g1 = std::min<int64_t>((((int64_t)blockIdx.x + 1) * nchunks / gridDim.x) * kBlock, ngroups);
+#if TFG_WG_PERM  // measurement switch: consecutive workgroups take chunks TFG_WG_PERM apart (a permutation
+                 // when gridDim is not a multiple of it), so the resident ones spread over the whole shard
+  const int64_t wg = ((int64_t)blockIdx.x * TFG_WG_PERM) % gridDim.x;
+#else
+  const int64_t wg = blockIdx.x;
+#endif
+  const int64_t g0 = (wg * nchunks / gridDim.x) * kBlock;
+  const int64_t g1 = std::min<int64_t>(((wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
   const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad);
 
