@@ -10,9 +10,9 @@ forcing in and its outputs out, to its own history slot: hist_depth = fuse, so
 no output write can be absorbed by a cache rewrite).
 
 Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
-HBM-resident frames, fp32 engine (fp64 state), 96 steps per launch (HBM
-footprint ~210 GB of the 288 GB: 24 forcing frames 32 GB, 96 output slots
-155 GB, 72-slot snowfall window 19 GB, state and geometry 6 GB).  Shards of
+HBM-resident frames, fp32 engine (fp64 state), 128 steps per launch (HBM
+footprint ~266 GB of the 288 GB: 24 forcing frames 32 GB, 128 output slots
+206 GB, 72-slot snowfall window 19 GB, state and geometry 9 GB).  Shards of
 2^25 cells or fewer (the N >= 2 slabs) fuse 192 steps per launch (auto_fuse).
 
 --gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
@@ -22,7 +22,7 @@ There is no data-path collective; value = all cells x steps / max-over-ranks
 time between barriers.
 
 The timed region is a whole number of fused launches, at least MIN_LAUNCHES,
-covering --steps, and (with the automatic depth) a multiple of 192 steps, so
+covering --steps, and (with the automatic depth) a multiple of 384 steps, so
 every N times the same steps of the same grid; the JSON carries
 `steps_requested` beside the timed `steps`.
 
@@ -67,12 +67,14 @@ MIN_LAUNCHES = 6
 # 0.5-3.6 ms long at every shape and warm-up length (profiles/r3c_slab_skew_study.jsonl,
 # profiles/r3f_slab_depth_study.jsonl); over 6 launches it weighs ~1 % on the
 # 1024 x 8192 slab instead of ~2 % over 3.
-# auto launch depth: 96 steps for shards above 2^25 cells (the 8192^2 grid: the
-# 96 output slots already take 155 GB of HBM), 192 below (the strong-scaling
-# slabs: a deeper launch amortises the state-in / state-out phases of each
-# launch; 1024 x 8192 cells 106 -> 112 G cell-updates/s, profiles/r2_fuse_slabs.json)
-FUSE_BIG, FUSE_SMALL, FUSE_SPLIT_CELLS = 96, 192, 1 << 25
-STEP_QUANTUM = 192  # timed steps are a multiple of both depths: the same total work at every N
+# auto launch depth: 128 steps for shards above 2^25 cells (the 8192^2 grid: the
+# 128 output slots take 206 GB of HBM, the whole footprint 266 GB; 96-step
+# launches ran 1.0 % slower on the same box, profiles/r3q_fuse128.log), 192 below
+# (the strong-scaling slabs: a deeper launch amortises the state-in / state-out
+# phases of each launch; 1024 x 8192 cells 106 -> 112 G cell-updates/s,
+# profiles/r2_fuse_slabs.json)
+FUSE_BIG, FUSE_SMALL, FUSE_SPLIT_CELLS = 128, 192, 1 << 25
+STEP_QUANTUM = 384  # timed steps are a multiple of both depths: the same total work at every N
 
 
 def auto_fuse(cells: int) -> int:
@@ -87,12 +89,14 @@ def warmup_steps(requested: int, fuse: int) -> int:
 
 def timed_steps(requested: int, fuse: int, explicit: bool) -> int:
     """Whole launches covering `requested`, at least MIN_LAUNCHES of them.  With
-    the automatic depth the count is a multiple of STEP_QUANTUM and at least
-    MIN_LAUNCHES x 192, so N = 1 (96-step launches) and N > 1 (192-step
-    launches) time the same number of steps of the same grid."""
+    the automatic depth the count is a multiple of STEP_QUANTUM covering at
+    least MIN_LAUNCHES launches of the deepest automatic depth, so N = 1
+    (128-step launches) and N > 1 (192-step launches) time the same number of
+    steps of the same grid."""
     if explicit:
         return max(MIN_LAUNCHES, -(-requested // fuse)) * fuse
-    return max(MIN_LAUNCHES, -(-requested // STEP_QUANTUM)) * STEP_QUANTUM
+    need = max(requested, MIN_LAUNCHES * max(FUSE_BIG, FUSE_SMALL))
+    return -(-need // STEP_QUANTUM) * STEP_QUANTUM
 
 BASE_CFG = {
     "site_prefix": "synthetic", "forcing_file": "synthetic", "dt": 1, "start_time": "2013032000",
