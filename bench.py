@@ -74,6 +74,7 @@ MIN_LAUNCHES = 6
 # phases of each launch; 1024 x 8192 cells 106 -> 112 G cell-updates/s,
 # profiles/r2_fuse_slabs.json)
 FUSE_BIG, FUSE_SMALL, FUSE_SPLIT_CELLS = 128, 192, 1 << 25
+FUSE_FALLBACK = 96  # if a device cannot hold FUSE_BIG output slots (main())
 STEP_QUANTUM = 384  # timed steps are a multiple of both depths: the same total work at every N
 
 
@@ -347,6 +348,7 @@ def main():
     import torch.distributed as dist
 
     from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier._native import NativeError
     from topoflow_glacier.engine import GlacierEngine
     from topoflow_glacier.sharding import allreduce_diagnostics
     from topoflow_glacier.synthetic import diurnal_table
@@ -376,8 +378,19 @@ def main():
         args.fuse = auto_fuse(plan["rows_max"] * args.nx)
     cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
     n_catch = args.catchments + 1 if args.catchments > 0 else 1
-    eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
-                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+    depth_note = None
+    try:
+        eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+                            hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+    except NativeError as e:
+        # the 128-step history takes 206 GB of the 266 GB footprint at 8192^2: where a
+        # device cannot hold it, the round-2 depth (96 steps, 212 GB) times the same steps
+        if fuse_explicit or args.fuse != FUSE_BIG or "memory" not in str(e).lower():
+            raise
+        depth_note = f"{FUSE_BIG}-step history did not fit ({e}); fused {FUSE_FALLBACK} steps"
+        args.fuse = FUSE_FALLBACK
+        eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+                            hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
     eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
     if args.catchments > 0:
         eng.set_field("catch_id", catchment_blocks(row0, rows, ny_global, args.nx, args.catchments))
@@ -481,6 +494,7 @@ def main():
             "ranks": ranks,
             "steps": steps,
             "steps_requested": args.steps,
+            "depth_note": depth_note,
             "steps_note": None if steps == args.steps else (
                 f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps) to cover the "
                 f"{args.steps} requested: a launch keeps each cell's state in registers across its steps, so the "
