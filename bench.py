@@ -422,6 +422,7 @@ def main():
     warm_steps = warmup_steps(args.warmup, args.fuse)
     eng.run(warm_steps)
     barrier()
+    ns_before = eng.nan_safe_launches() if args.engine == "float32" else 0
     # Whole fused launches, and at least MIN_LAUNCHES of them, so that a short
     # --steps still gives a multi-launch timed region; the JSON carries the
     # requested count beside the timed one.
@@ -459,6 +460,8 @@ def main():
     mean_launch_s = float(launch_ms.mean()) / 1e3
     bytes_launch = cells * launch_bytes_per_cell(args.fuse)
     achieved = bytes_launch / mean_launch_s / 1e9
+    # launches of the timed region that ran the fp32 step's NaN-safe form (0: the clean form was timed)
+    ns_timed = (eng.nan_safe_launches() - ns_before) if args.engine == "float32" else None
     # the host-fed leg and the CPU baseline run on rank 0 at N=1 only (BASELINE contract)
     pcie = pcie_inclusive(eng, args, torch) if world == 1 and args.pcie else None
     eng.close()
@@ -495,6 +498,8 @@ def main():
             "steps": steps,
             "steps_requested": args.steps,
             "depth_note": depth_note,
+            # launches of the timed region that ran the fp32 step's NaN-safe form (0: the clean form was timed)
+            "nan_safe_timed_launches": ns_timed,
             "steps_note": None if steps == args.steps else (
                 f"timed {n_launch} whole {args.fuse}-step fused launches ({steps} steps) to cover the "
                 f"{args.steps} requested: a launch keeps each cell's state in registers across its steps, so the "

@@ -75,6 +75,7 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert d["launches"]["count"] == 6 and d["launches"]["ms_min"] <= d["launches"]["ms_mean"] <= d["launches"]["ms_max"]
     assert d["value"] > 0 and d["higher_is_better"] is True
     assert d["config"]["workload"] and d["dtype"] == "f32" and d["scaling"] == "strong"
+    assert d["nan_safe_timed_launches"] == 0  # synthetic data is finite: the clean step form was timed
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-12
