@@ -974,6 +974,9 @@ int tfg_device_count(int* count) {
   return TFG_OK;
 }
 
+// Plane-stride skew of large shards (tfg_create), a multiple of the 256-cell chunk.
+constexpr int64_t kPlaneSkew = 512;
+
 int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int device, int n_frames,
                int hist_depth, int n_catch, tfg_handle** out) {
   if (!p || !out) return fail(nullptr, TFG_ERR_ARG, "null params/out");
@@ -1000,9 +1003,17 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->nx = nx;
   h->n = ny * nx;
   h->n_pad = round_up(h->n, 64);
-  // TFG_PLANE_SKEW (measurement only): plane stride n_pad + skew cells, so that
-  // the planes of a power-of-two shard do not sit at power-of-two distances
-  if (const char* e = std::getenv("TFG_PLANE_SKEW")) h->n_pad += round_up(std::max<int64_t>(0, atoll(e)), 64);
+  // Plane stride n_pad = round_up(n, 64) + kPlaneSkew cells for shards of 2^20
+  // cells or more, so that the planes of a power-of-two shard do not sit at
+  // power-of-two distances.  With the plain stride the streaming rate depended
+  // on where the allocator put the buffers: 105-115 G cell-updates/s over fresh
+  // allocations of one 4096^2 shard in one process, 113.8-116.0 with 512 cells
+  // (2 KB) of skew; 1024 x 8192: 111.9-114.1 against 113.7-115.2; 8192^2:
+  // 116.4-117.4 against 117.2-117.5 (tests/diagnostics/alloc_variance.py,
+  // DESIGN.md section 5).  TFG_PLANE_SKEW=<cells> overrides it (measurement).
+  int64_t skew = h->n_pad >= ((int64_t)1 << 20) ? kPlaneSkew : 0;
+  if (const char* e = std::getenv("TFG_PLANE_SKEW")) skew = round_up(std::max<int64_t>(0, atoll(e)), 64);
+  h->n_pad += skew;
   if (h->n_pad * 8 >= (int64_t)1 << 32) {
     h->err = "shard too large: ny*nx must stay below 2^29 cells per device (32-bit field offsets)";
     g_err = h->err;
