@@ -13,7 +13,8 @@ Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
 HBM-resident frames, fp32 engine (fp64 state), 128 steps per launch (HBM
 footprint ~266 GB of the 288 GB: 24 forcing frames 32 GB, 128 output slots
 206 GB, 72-slot snowfall window 19 GB, state and geometry 9 GB).  Shards of
-2^25 cells or fewer (the N >= 2 slabs) fuse 192 steps per launch (auto_fuse).
+2^25 cells or fewer fuse 192 steps per launch (N = 2), 2^24 or fewer 384
+(N >= 4; auto_fuse).
 
 --gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
 is row-partitioned over the N ranks (strong scaling, BASELINE config 4: 1024 x
@@ -67,19 +68,23 @@ MIN_LAUNCHES = 6
 # 0.5-3.6 ms long at every shape and warm-up length (profiles/r3c_slab_skew_study.jsonl,
 # profiles/r3f_slab_depth_study.jsonl); over 6 launches it weighs ~1 % on the
 # 1024 x 8192 slab instead of ~2 % over 3.
-# auto launch depth: 128 steps for shards above 2^25 cells (the 8192^2 grid: the
-# 128 output slots take 206 GB of HBM, the whole footprint 266 GB; 96-step
-# launches ran 1.0 % slower on the same box, profiles/r3q_fuse128.log), 192 below
-# (the strong-scaling slabs: a deeper launch amortises the state-in / state-out
-# phases of each launch; 1024 x 8192 cells 106 -> 112 G cell-updates/s,
-# profiles/r2_fuse_slabs.json)
-FUSE_BIG, FUSE_SMALL, FUSE_SPLIT_CELLS = 128, 192, 1 << 25
+# auto launch depth by shard size, as deep as ~210 GB of output slots allow
+# (hist_depth = launch depth): 128 steps above 2^25 cells (the 8192^2 grid: the
+# 128 slots take 206 GB, the whole footprint 266 GB; 96-step launches ran 1.0 %
+# slower on the same box, profiles/r3q_fuse128.log), 192 above 2^24 (4096 x 8192,
+# N = 2: 154 GB), 384 at 2^24 and below (N >= 4: a deeper launch amortises the
+# per-launch cost; 1024 x 8192 with the plane skew 112.6-113.6 -> 115.2-115.7 G
+# cell-updates/s from 192 to 384, profiles/r3ab_slab_k.log)
+FUSE_BIG, FUSE_MID, FUSE_SMALL = 128, 192, 384
+FUSE_SPLIT_CELLS, FUSE_SMALL_CELLS = 1 << 25, 1 << 24
 FUSE_FALLBACK = 96  # if a device cannot hold FUSE_BIG output slots (main())
-STEP_QUANTUM = 384  # timed steps are a multiple of both depths: the same total work at every N
+STEP_QUANTUM = 384  # timed steps are a multiple of every depth: the same total work at every N
 
 
 def auto_fuse(cells: int) -> int:
-    return FUSE_BIG if cells > FUSE_SPLIT_CELLS else FUSE_SMALL
+    if cells > FUSE_SPLIT_CELLS:
+        return FUSE_BIG
+    return FUSE_MID if cells > FUSE_SMALL_CELLS else FUSE_SMALL
 
 
 def warmup_steps(requested: int, fuse: int) -> int:
@@ -92,11 +97,11 @@ def timed_steps(requested: int, fuse: int, explicit: bool) -> int:
     """Whole launches covering `requested`, at least MIN_LAUNCHES of them.  With
     the automatic depth the count is a multiple of STEP_QUANTUM covering at
     least MIN_LAUNCHES launches of the deepest automatic depth, so N = 1
-    (128-step launches) and N > 1 (192-step launches) time the same number of
+    (128-step launches), N = 2 (192) and N >= 4 (384) time the same number of
     steps of the same grid."""
     if explicit:
         return max(MIN_LAUNCHES, -(-requested // fuse)) * fuse
-    need = max(requested, MIN_LAUNCHES * max(FUSE_BIG, FUSE_SMALL))
+    need = max(requested, MIN_LAUNCHES * max(FUSE_BIG, FUSE_MID, FUSE_SMALL))
     return -(-need // STEP_QUANTUM) * STEP_QUANTUM
 
 BASE_CFG = {

@@ -37,15 +37,16 @@ def test_default_shard_plan_is_config4_strong_scaling(world):
     assert plans[0]["scaling"] == "strong"  # one label for the driver's whole N = 1, 2, 4, 8 series
 
 
-@pytest.mark.parametrize("world,fuse", [(1, 128), (2, 192), (4, 192), (8, 192)])
+@pytest.mark.parametrize("world,fuse", [(1, 128), (2, 192), (4, 384), (8, 384)])
 def test_driver_command_times_the_same_work_at_every_n(world, fuse):
-    """`--steps 20`: whole launches, >= 6, and the same 1152 steps at every N
-    (128-step launches for the whole 8192^2 grid, 192-step ones for the slabs)."""
+    """`--steps 20`: whole launches, >= 6, and the same 2304 steps at every N
+    (128-step launches for the whole 8192^2 grid, 192 for 4096 x 8192, 384 for
+    the smaller slabs)."""
     bench, args = _args("--gpus", str(world), "--steps", "20", "--warmup", "5")
     plan = bench.shard_plan(args, world, 0)
     k = bench.auto_fuse(plan["rows_max"] * args.nx)
     steps = bench.timed_steps(args.steps, k, explicit=False)
-    assert k == fuse and steps == 1152 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
+    assert k == fuse and steps == 2304 and steps % k == 0 and steps // k >= bench.MIN_LAUNCHES
     assert bench.timed_steps(48, 24, explicit=True) == 144  # an explicit --fuse: >= 6 launches of it
     # the driver's --warmup 5 still warms one whole launch of the timed depth
     assert bench.warmup_steps(args.warmup, k) == k and bench.warmup_steps(400, k) == 400
