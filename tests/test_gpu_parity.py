@@ -272,6 +272,36 @@ def test_satterlund_synthetic_vs_oracle():
 
 # ---------------------------------------------------------------- invariances
 @pytest.mark.parametrize("engine", ["float32", "float64"])
+def test_plane_stride_is_invisible(engine, monkeypatch):
+    """Shards of 2^20 cells or more get a plane stride of n + 512 cells
+    (tfg_create, kPlaneSkew); the padding changes no result: a 1024 x 1024
+    shard with the default stride, with TFG_PLANE_SKEW=0 and with a 4096-cell
+    skew gives the same outputs, state and diagnostics bit for bit."""
+    runs = []
+    for skew in (None, "0", "4096"):
+        if skew is None:
+            monkeypatch.delenv("TFG_PLANE_SKEW", raising=False)
+        else:
+            monkeypatch.setenv("TFG_PLANE_SKEW", skew)
+        e = make_engine(BASE_CFG, 1024, 1024, engine, n_frames=24, hist_depth=24, fuse_steps=24)
+        try:
+            e.fill_synthetic(5, synthetic_inputs(5, 1, 1, 24)[1])
+            e.run(48)
+            e.sync()
+            outs = {v: np.stack([e.get_field(v, index=k) for k in range(24)]) for v in HIST}
+            state = {v: e.get_field(v) for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")}
+            runs.append((outs, state, e.diagnostics()))
+        finally:
+            e.close()
+    for o, st, dg in runs[1:]:
+        for v in HIST:
+            assert np.array_equal(o[v], runs[0][0][v]), v
+        for v in st:
+            assert np.array_equal(st[v], runs[0][1][v]), v
+        assert np.array_equal(dg, runs[0][2])
+
+
+@pytest.mark.parametrize("engine", ["float32", "float64"])
 def test_fusion_is_invisible(engine):
     """fuse_steps=1 (one launch per step) and fused launches give identical bits."""
     g = load_golden("grid64")
