@@ -596,6 +596,7 @@ struct tfg_handle {
   int64_t* tot = nullptr;
   int32_t* ring = nullptr;
   void* hist = nullptr;
+  void* arena = nullptr;         // one allocation holding forc, ring and hist (TFG_ARENA), or null
   double* diag = nullptr;        // [n_catch][6]
   double* slab = nullptr;        // [max_blocks][n_catch][6]
   float* d_diurnal = nullptr;
@@ -1068,7 +1069,24 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {(void**)&h->slab, (size_t)h->max_blocks * n_catch * 6 * 8},
       {(void**)&h->d_flag, 4},
   };
+  // TFG_ARENA=1 (measurement switch): the streamed planes -- forcing frames,
+  // window slots and output slots -- in one allocation, so that their
+  // relative placement is fixed by the layout rather than by the allocator.
+  if (const char* e = std::getenv("TFG_ARENA"); e && atoi(e) != 0) {
+    const size_t fb = (size_t)n_frames * kNumForc * np * rs, rb = (size_t)p->ring_len * np * 4,
+                 hb = (size_t)hist_depth * kNumHist * np * rs;
+    hipError_t err = hipMalloc(&h->arena, fb + rb + hb);
+    if (err != hipSuccess) {
+      h->err = std::string("hipMalloc(") + std::to_string(fb + rb + hb) + " B) failed: " + hipGetErrorString(err);
+      return bail(TFG_ERR_HIP);
+    }
+    if (hipMemsetAsync(h->arena, 0, fb + rb + hb, h->stream) != hipSuccess) { h->err = "hipMemset failed"; return bail(TFG_ERR_HIP); }
+    h->forc = h->arena;
+    h->ring = reinterpret_cast<int32_t*>(static_cast<char*>(h->arena) + fb);
+    h->hist = static_cast<char*>(h->arena) + fb + rb;
+  }
   for (auto& a : allocs) {
+    if (*a.p) continue;  // placed in the arena
     hipError_t e = hipMalloc(a.p, a.bytes);
     if (e != hipSuccess) {
       h->err = std::string("hipMalloc(") + std::to_string(a.bytes) + " B) failed: " + hipGetErrorString(e);
@@ -1088,6 +1106,11 @@ int tfg_destroy(tfg_handle* h) {
   // work queued on a caller's stream (tfg_set_stream) may still use the buffers
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
+  if (h->arena) {  // forc, ring and hist are views into it
+    (void)hipFree(h->arena);
+    h->arena = h->forc = h->hist = nullptr;
+    h->ring = nullptr;
+  }
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
                   h->flow_halo, h->flow_edges, h->flow_red, h->qc, h->cond_halo, h->cond_edges,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
