@@ -204,6 +204,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_WG_PERM
 #define TFG_WG_PERM 0
 #endif
+#ifndef TFG_START_STAGGER
+#define TFG_START_STAGGER 0
+#endif
 #ifndef TFG_MIN_WAVES
 #define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
 #endif
@@ -230,6 +233,13 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
   for (int i = threadIdx.x; i < kWaves * nb; i += kBlock) lds_bins[i] = ((i % 6) == 5) ? -INFINITY : 0.0;
   __syncthreads();
   double* wbins = lds_bins + (threadIdx.x >> 6) * nb;
+#if TFG_START_STAGGER  // measurement switch: the first round of resident workgroups starts at staggered
+                       // times, 0 .. TFG_START_STAGGER-1 sleeps of ~3.4 us, spread over every XCD
+  if (blockIdx.x < 1024) {
+    const int d = (int)((blockIdx.x >> 3) % TFG_START_STAGGER);
+    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+#endif
 
   const int64_t n_pad = a.n_pad;
   const int64_t ngroups = n_pad / C;
