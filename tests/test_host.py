@@ -239,6 +239,39 @@ def test_bmi_surface_without_gpu():
     assert m.get_value("land_surface_air__temperature", np.zeros(1))[0] == 273.15
 
 
+def test_bmi_grid_topology_of_the_raster():
+    """The uniform raster's coordinates and quad topology (additive BMI 2.0
+    methods the reference leaves unimplemented)."""
+    from types import SimpleNamespace
+
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    m = BmiTopoflowGlacier()
+    m.ny, m.nx, m.n_cells = 3, 4, 12
+    m.cfg = SimpleNamespace(da=0.25)  # km^2: 500 m cells
+    ny, nx = 3, 4
+    assert m.get_grid_node_count(0) == 12 and m.get_grid_size(0) == 12
+    np.testing.assert_array_equal(m.get_grid_x(0, np.zeros(nx)), [0, 500, 1000, 1500])
+    np.testing.assert_array_equal(m.get_grid_y(0, np.zeros(ny)), [0, 500, 1000])
+    with pytest.raises(NotImplementedError):
+        m.get_grid_z(0, np.zeros(1))
+    ne, nf = m.get_grid_edge_count(0), m.get_grid_face_count(0)
+    assert (ne, nf) == (ny * (nx - 1) + (ny - 1) * nx, (ny - 1) * (nx - 1))
+    en = m.get_grid_edge_nodes(0, np.zeros(2 * ne, np.int64)).reshape(ne, 2)
+    r, c = np.divmod(en, nx)
+    assert np.all(np.abs(r[:, 0] - r[:, 1]) + np.abs(c[:, 0] - c[:, 1]) == 1)  # neighbours
+    assert len({tuple(sorted(e)) for e in en.tolist()}) == ne  # each edge once
+    fn = m.get_grid_face_nodes(0, np.zeros(4 * nf, np.int64)).reshape(nf, 4)
+    fe = m.get_grid_face_edges(0, np.zeros(4 * nf, np.int64)).reshape(nf, 4)
+    assert np.all(m.get_grid_nodes_per_face(0, np.zeros(nf, np.int64)) == 4)
+    x, y = fn % nx, fn // nx
+    area2 = (x * np.roll(y, -1, axis=1) - np.roll(x, -1, axis=1) * y).sum(axis=1)
+    assert np.all(area2 == 2)  # unit squares, counter-clockwise
+    for k in range(4):  # edge k of a face joins its nodes k and k + 1
+        a, b = fn[:, k], fn[:, (k + 1) % 4]
+        assert all(sorted(en[e]) == sorted((i, j)) for e, i, j in zip(fe[:, k], a, b))
+
+
 # ----------------------------------------------------------------- synthetic
 def test_synthetic_mirror_is_deterministic_and_in_range():
     from topoflow_glacier.synthetic import diurnal_table, hash_u01, synthetic_cells

@@ -2,7 +2,8 @@
 
 The CSDMS ``bmipy.Bmi`` ABC is used when it is installed; otherwise a plain
 object base stands in (bmipy carries no arithmetic).  Methods this model does
-not support raise NotImplementedError, as in the reference.
+not support raise NotImplementedError, as in the reference; the grid
+topology the reference leaves unimplemented there is BmiTopoflowGlacier's.
 """
 
 from __future__ import annotations
@@ -29,34 +30,3 @@ class BmiBase(_Bmi):
 
     def get_var_type(self, name) -> str:
         return str(self.get_value_ptr(name).dtype)
-
-    # grid topology beyond the uniform raster is not modelled
-    def get_grid_edge_count(self, grid):
-        raise NotImplementedError()
-
-    def get_grid_edge_nodes(self, grid, edge_nodes):
-        raise NotImplementedError()
-
-    def get_grid_face_count(self, grid):
-        raise NotImplementedError()
-
-    def get_grid_face_edges(self, grid, face_edges):
-        raise NotImplementedError()
-
-    def get_grid_face_nodes(self, grid, face_nodes):
-        raise NotImplementedError()
-
-    def get_grid_node_count(self, grid):
-        raise NotImplementedError()
-
-    def get_grid_nodes_per_face(self, grid, nodes_per_face):
-        raise NotImplementedError()
-
-    def get_grid_x(self, grid, x):
-        raise NotImplementedError()
-
-    def get_grid_y(self, grid, y):
-        raise NotImplementedError()
-
-    def get_grid_z(self, grid, z):
-        raise NotImplementedError()

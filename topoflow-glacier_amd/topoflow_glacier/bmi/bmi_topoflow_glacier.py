@@ -600,6 +600,65 @@ class BmiTopoflowGlacier(BmiBase):
     def get_grid_type(self, grid: int) -> str:
         return "uniform_rectilinear"
 
+    # Node coordinates and quad topology of the uniform raster (BMI 2.0), for
+    # callers that walk every grid the same way.  The reference leaves these
+    # unimplemented (bmi_base.py); they are additive.  Nodes are numbered row
+    # by row (index = row * nx + col, the layout of every value array); edges
+    # are the nx - 1 x-edges of each row, then the nx y-edges of each row pair;
+    # faces are the cells between four nodes, counter-clockwise from the
+    # lower-left node, with edges in the same order.
+    def _axis(self, k: int) -> np.ndarray:
+        sp = self.get_grid_spacing(0, np.empty(2))
+        n = (self.ny, self.nx)[k]
+        return np.arange(n, dtype=np.float64) * sp[k]
+
+    def get_grid_x(self, grid: int, x):
+        x[:] = self._axis(1)
+        return x
+
+    def get_grid_y(self, grid: int, y):
+        y[:] = self._axis(0)
+        return y
+
+    def get_grid_z(self, grid: int, z):
+        raise NotImplementedError("the grid is two-dimensional")
+
+    def get_grid_node_count(self, grid: int) -> int:
+        return self.get_grid_size(grid)
+
+    def get_grid_edge_count(self, grid: int) -> int:
+        return self.ny * (self.nx - 1) + (self.ny - 1) * self.nx
+
+    def get_grid_face_count(self, grid: int) -> int:
+        return (self.ny - 1) * (self.nx - 1)
+
+    def get_grid_edge_nodes(self, grid: int, edge_nodes):
+        ny, nx = self.ny, self.nx
+        node = np.arange(ny * nx).reshape(ny, nx)
+        ex = np.stack([node[:, :-1], node[:, 1:]], axis=-1).reshape(-1, 2)
+        ey = np.stack([node[:-1, :], node[1:, :]], axis=-1).reshape(-1, 2)
+        edge_nodes[:] = np.concatenate([ex, ey]).ravel()
+        return edge_nodes
+
+    def get_grid_face_nodes(self, grid: int, face_nodes):
+        node = np.arange(self.ny * self.nx).reshape(self.ny, self.nx)
+        f = np.stack([node[:-1, :-1], node[:-1, 1:], node[1:, 1:], node[1:, :-1]], axis=-1)
+        face_nodes[:] = f.ravel()
+        return face_nodes
+
+    def get_grid_face_edges(self, grid: int, face_edges):
+        ny, nx = self.ny, self.nx
+        n_ex = ny * (nx - 1)
+        ex = np.arange(n_ex).reshape(ny, nx - 1)
+        ey = n_ex + np.arange((ny - 1) * nx).reshape(ny - 1, nx)
+        f = np.stack([ex[:-1, :], ey[:, 1:], ex[1:, :], ey[:, :-1]], axis=-1)
+        face_edges[:] = f.ravel()
+        return face_edges
+
+    def get_grid_nodes_per_face(self, grid: int, nodes_per_face):
+        nodes_per_face[:] = 4
+        return nodes_per_face
+
     # ------------------------------------------------------------------ time
     def get_start_time(self) -> float:
         return 0.0
