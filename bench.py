@@ -544,8 +544,8 @@ def main():
                 "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
                 "kernel_ms_per_launch": float(launch_ms.mean()),
                 "note": None if args.engine == "float32" else (
-                    "the fp64 engine is compute-bound, not HBM-bound: its step issues 1450 VALU instructions per "
-                    "wave and cell-step, 90 % of the vector pipe at 4 waves per SIMD (profiles/r2r_issue_counters.json); "
+                    "the fp64 engine is compute-bound, not HBM-bound: its step issues 1088 VALU instructions per "
+                    "wave and cell-step, 81 % of the vector pipe at 4 waves per SIMD (profiles/r3z_issue_counters.json); "
                     "frac is its HBM share only"),
             },
             "cpu_baseline": cpu,
