@@ -28,8 +28,21 @@ __device__ __forceinline__ void splat(float& o, float a) { o = a; }
 __device__ __forceinline__ void splat(float2& o, float a) { o = make_float2(a, a + 1.0f); }
 __device__ __forceinline__ void splat(float4& o, float a) { o = make_float4(a, a + 1.0f, a + 2.0f, a + 3.0f); }
 
-// V floats (V adjacent cells) per lane per plane; NT: non-temporal stores
-template <int R, int W, int V, bool NT = false>
+// Store cache policy of the 4-byte stores (POL > 0, V = 1): the gfx950
+// global_store_dword bits, written out in asm (the compiler emits only plain and nt).
+template <int POL>
+__device__ __forceinline__ void store_pol(float* p, float v) {
+  if constexpr (POL == 1) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 2) asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 3) asm volatile("global_store_dword %0, %1, off sc1 nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 4) asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 5) asm volatile("global_store_dword %0, %1, off sc0 nt" ::"v"(p), "v"(v) : "memory");
+  else if constexpr (POL == 6) asm volatile("global_store_dword %0, %1, off sc0" ::"v"(p), "v"(v) : "memory");
+}
+
+// V floats (V adjacent cells) per lane per plane; NT: non-temporal stores;
+// POL: a store cache policy of store_pol instead
+template <int R, int W, int V, bool NT = false, int POL = 0>
 __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float* __restrict__ out, uint32_t n,
                                              int steps, int frames, uint32_t ps) {
   using T = typename Vec<V>::T;
@@ -50,7 +63,8 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float
         T o;
         splat(o, acc + (float)w);
         T* dst = reinterpret_cast<T*>(fo + (size_t)w * ps) + i;
-        if constexpr (NT) __builtin_nontemporal_store(o, dst);
+        if constexpr (POL > 0) { static_assert(V == 1, "policy stores are 4 B"); store_pol<POL>((float*)dst, hsum(o)); }
+        else if constexpr (NT) __builtin_nontemporal_store(o, dst);
         else *dst = o;
       }
     }
@@ -85,20 +99,20 @@ __global__ __launch_bounds__(256) void k_mix_il(const float* __restrict__ in, fl
 static int g_blocks = 256 * 8;
 static uint32_t g_skew = 0;
 
-template <int R, int W, int V = 1, bool NT = false>
+template <int R, int W, int V = 1, bool NT = false, int POL = 0>
 void run(const char* name, float* in, float* out, uint32_t n, int steps, int frames) {
   hipEvent_t a, b;
   CHECK(hipEventCreate(&a));
   CHECK(hipEventCreate(&b));
   const int blocks = g_blocks;
   const uint32_t ps = n + g_skew;
-  k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames, ps);  // warm-up
+  k_mix<R, W, V, NT, POL><<<blocks, 256>>>(in, out, n, steps, frames, ps);  // warm-up
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int rep = 0; rep < 5; ++rep) {
     CHECK(hipEventRecord(a));
-    k_mix<R, W, V, NT><<<blocks, 256>>>(in, out, n, steps, frames, ps);
+    k_mix<R, W, V, NT, POL><<<blocks, 256>>>(in, out, n, steps, frames, ps);
     CHECK(hipEventRecord(b));
     CHECK(hipEventSynchronize(b));
     float ms;
@@ -290,6 +304,24 @@ int main(int argc, char** argv) {
     run_il<6, 7, 1024>("k_fused step mix, 1024-cell block interleave", in, out, n, steps, frames);
     run<6, 7>("k_fused step mix (6 read, 7 write), planar", in, out, n, steps, frames);
     run_il<6, 7, 64>("k_fused step mix, 64-cell block interleave", in, out, n, steps, frames);
+    CHECK(hipFree(in));
+    CHECK(hipFree(out));
+    return 0;
+  }
+  if (argc > 5 && std::string(argv[5]) == "pol") {  // store cache-policy experiment only
+    for (int rep = 0; rep < 2; ++rep) {
+      run<6, 7, 1, false>("k_fused step mix, plain stores", in, out, n, steps, frames);
+      run<6, 7, 1, true>("k_fused step mix, nt stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 1>("k_fused step mix, sc1 stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 2>("k_fused step mix, sc0 sc1 stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 3>("k_fused step mix, sc1 nt stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 4>("k_fused step mix, sc0 sc1 nt stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 5>("k_fused step mix, sc0 nt stores", in, out, n, steps, frames);
+      run<6, 7, 1, false, 6>("k_fused step mix, sc0 stores", in, out, n, steps, frames);
+    }
+    run<0, 7, 1, true>("write only, nt stores", in, out, n, steps, frames);
+    run<0, 7, 1, false, 1>("write only, sc1 stores", in, out, n, steps, frames);
+    run<0, 7, 1, false, 4>("write only, sc0 sc1 nt stores", in, out, n, steps, frames);
     CHECK(hipFree(in));
     CHECK(hipFree(out));
     return 0;
