@@ -10,7 +10,10 @@
   * config 5's per-GPU slab: rows 6144..8191 of the 16384 x 16384 grid over 8
     GPUs (2048 x 16384 cells), dt = 0.25 h (a 288-slot snowfall window), 43
     catchments (256 x 256-cell blocks, ids mod 43), 384 steps in four 96-step
-    launches (longer than the window, so slots expire).
+    launches (longer than the window, so slots expire);
+  * the largest shard the library accepts: 16383 x 32769 cells (536.9 M, an odd
+    count, so the last wave is ragged), where the fp64 state planes' 32-bit
+    lane byte offsets reach 4.29e9, just below 2^32.
 
 The oracle cannot run tens of millions of cells, so each case checks what
 holds at any size:
@@ -41,7 +44,12 @@ CONFIGS = {
     "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 192, 96, 0),  # the bench's launch shape
     "config3_4096sq": (4096, 4096, 0, 4096, 1.0, 48, 24, 0),
     "config5_slab_2048x16384_dt0.25_43catch": (2048, 16384, 6144, 16384, 0.25, 384, 96, 43),
+    # the largest shard tfg_create accepts (n_pad * 8 < 2^32: fp64 planes at
+    # 32-bit lane byte offsets up to 4.29e9), ragged (ny * nx odd), dt = 2 h (a
+    # 36-slot window) and 2 forcing frames so that it fits one GPU (~220 GB)
+    "max_shard_16383x32769_dt2": (16383, 32769, 0, 16383, 2.0, 8, 4, 0),
 }
+FRAMES = {"max_shard_16383x32769_dt2": 2}  # forcing frames cycled (default 24)
 
 
 def _sample_cells(rng, n, nx):
@@ -64,7 +72,7 @@ def _catchments(row0, rows, nx, k):
     return ((r + c) % k).astype(np.int32).reshape(-1)
 
 
-def _run(torch, cfg, shape, cells, cid):
+def _run(torch, cfg, shape, cells, cid, nf=24):
     """One run of a shard: sampled outputs [steps][cells], runoff sum, storage
     sums before and after, final h_swe on device, diagnostics, and (with
     catchments) per-catchment bincounts of the engine's own outputs."""
@@ -72,7 +80,8 @@ def _run(torch, cfg, shape, cells, cid):
 
     ny, nx, row0, _, dt, steps, fuse, ncatch = shape
     n = ny * nx
-    e = make_engine(cfg, ny, nx, "float32", n_frames=24, hist_depth=fuse, fuse_steps=fuse, row0=row0,
+    torch.cuda.empty_cache()  # the largest shard needs the memory torch keeps cached
+    e = make_engine(cfg, ny, nx, "float32", n_frames=nf, hist_depth=fuse, fuse_steps=fuse, row0=row0,
                     n_catch=max(ncatch, 1))
 
     def dev(name, index, dtype):
@@ -80,7 +89,7 @@ def _run(torch, cfg, shape, cells, cid):
         return e.get_field_device(name, torch.empty(n, dtype=dtype, device="cuda:0"), index=index)
 
     try:
-        e.fill_synthetic(SEED, diurnal_table(24), nx_global=nx)
+        e.fill_synthetic(SEED, diurnal_table(nf), nx_global=nx)
         if ncatch:
             e.set_field("catch_id", cid)
             # per-cell sums over the run, binned by catchment once at the end
@@ -131,15 +140,16 @@ def test_full_size_sampled_parity_water_balance_and_determinism(name):
 
     shape = CONFIGS[name]
     ny, nx, row0, ny_global, dt, steps, fuse, ncatch = shape
+    nf = FRAMES.get(name, 24)
     cfg = dict(BASE_CFG, dt=dt)
     n = ny * nx
     cells = _sample_cells(np.random.default_rng(5), n, nx)
     cid = _catchments(row0, ny, nx, ncatch) if ncatch else None
-    gpu, runoff, s0, s1, swe1, dg, bins = _run(torch, cfg, shape, cells, cid)
+    gpu, runoff, s0, s1, swe1, dg, bins = _run(torch, cfg, shape, cells, cid, nf)
 
     # sampled parity against the oracle on the host mirror of the same fp32 inputs
-    syn = synthetic_cells(SEED, cells + row0 * nx, diurnal_table(24))
-    frames = np.arange(steps) % 24
+    syn = synthetic_cells(SEED, cells + row0 * nx, diurnal_table(nf))
+    frames = np.arange(steps) % nf
     forcing = {k: syn[k][frames].astype(np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
     static = {k: np.asarray(syn[s], np.float64) for k, s in (("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"),
               ("h0_snow", "h_snow"), ("h0_ice", "h_ice"), ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
@@ -184,7 +194,7 @@ def test_full_size_sampled_parity_water_balance_and_determinism(name):
         assert (dg[:, 3] > 0).all() and (dg[:, 0] > 0).all()
 
     # determinism: a second run, bit for bit
-    gpu2, runoff2, _, _, swe2, dg2, _ = _run(torch, cfg, shape, cells, cid)
+    gpu2, runoff2, _, _, swe2, dg2, _ = _run(torch, cfg, shape, cells, cid, nf)
     assert torch.equal(swe1, swe2) and np.array_equal(dg, dg2) and runoff == runoff2
     for v in HIST:
         assert np.array_equal(gpu[v], gpu2[v]), v
