@@ -379,6 +379,29 @@ def test_launches_longer_than_the_window_are_invisible(fuse, chunks, n_catch):
     assert np.array_equal(ref[3], got[3])  # all 72 window slots
 
 
+@pytest.mark.parametrize("engine", ["float32", "float64"])
+@pytest.mark.parametrize("dt", [24.0, 36.0, 72.0])
+def test_short_windows_fuse_like_single_steps(dt, engine):
+    """A fused launch requests each step's expiring window slot ahead of the
+    steps before it (two steps ahead in the fp32 engine, one in the fp64
+    engine), so it must not read a slot those steps still write.  dt = 24, 36
+    and 72 h give 3-, 2- and 1-slot windows (:296), the shortest the engines
+    fuse and the ones they step one launch at a time: 24-step launches equal
+    one launch per step, bit for bit (outputs, state, every window slot)."""
+    g = load_golden("grid64")
+    cfg = dict(g["cfg"], dt=dt)
+    nsteps = 40
+    ref = gpu_run_fields(cfg, g["static"], g["forcing"], 8, 8, engine, nsteps, fuse_steps=1, window=True)
+    got = gpu_run_fields(cfg, g["static"], g["forcing"], 8, 8, engine, nsteps, fuse_steps=24, window=True)
+    assert ref[3].shape[0] == int(72 / dt)
+    assert np.any(ref[3] != 0)  # snow fell into the window
+    for v in HIST:
+        assert np.array_equal(ref[0][v], got[0][v], equal_nan=True), v
+    for v in ref[1]:
+        assert np.array_equal(ref[1][v], got[1][v]), v
+    assert np.array_equal(ref[3], got[3])
+
+
 def test_row_shards_equal_whole_grid():
     """Row-block shards (row0 offsets) reproduce the unsharded grid exactly."""
     cfg = dict(BASE_CFG)

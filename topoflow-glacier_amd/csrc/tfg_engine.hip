@@ -1449,7 +1449,10 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   if (int rc = prepare_steps(h)) return rc;
   const int blocks = fused_blocks(h);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
-  const int fuse = h->ring_len > 1 ? h->fuse : 1;  // see the prefetch note in k_fused
+  // a fused launch reads each step's expiring window slot 1 (fp64 engine) or
+  // kPrefetchFast (fp32 engine) steps ahead: a shorter window runs unfused
+  // (see the prefetch note in k_fused)
+  const int fuse = h->ring_len > (h->engine == TFG_F32 ? kPrefetchFast : 1) ? h->fuse : 1;
   const bool one_cell = h->engine == TFG_F64 && h->n == 1 && !io.in;  // k_cell_run
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);

@@ -33,8 +33,10 @@ constexpr int kBlock = TFG_BLOCK;  // threads per workgroup
 #endif
 constexpr int kCellsPerThread = TFG_CELLS_PER_THREAD;  // adjacent cells per lane
 #ifndef TFG_PREFETCH_DEPTH
-#define TFG_PREFETCH_DEPTH 1  // time steps of forcing requested ahead
+#define TFG_PREFETCH_DEPTH 2  // time steps of forcing requested ahead by the fast engine (1 or 2)
 #endif
+constexpr int kPrefetchFast = TFG_PREFETCH_DEPTH;
+static_assert(kPrefetchFast == 1 || kPrefetchFast == 2, "TFG_PREFETCH_DEPTH is 1 or 2");
 constexpr int kWaves = kBlock / 64;
 constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
 constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
@@ -413,19 +415,14 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
         sstore(h + H_MTOT * n_pad, oR, o_mt[0]);
         sstore(h + H_RH * n_pad, oR, o_rh[0]);
       };
-#if TFG_PREFETCH_DEPTH == 2
-      Frame fa, fb, fc;
-      fetch(0, fa);
-      fetch(1, fb);
-      for (int k = 0; k < a.K; k += 3) {
-        fetch(k + 2, fc);
-        advance(k, fa);
-        fetch(k + 3, fa);
-        if (k + 1 < a.K) advance(k + 1, fb);
-        fetch(k + 4, fb);
-        if (k + 2 < a.K) advance(k + 2, fc);
-      }
-#else
+      // The fast engine requests two steps ahead (three register sets, loop
+      // unrolled by three, 127 VGPRs): +1.2-2.6 % at 1024^2, 2048^2 and 8192^2
+      // in same-box A/Bs against one step ahead.  Step
+      // k + 2's window slot is then read before steps k and k + 1 write theirs,
+      // so a fused launch needs ring_len > 2 (launch_steps runs shorter windows
+      // one step per launch).  The conduction (QC) and NaN-safe (NS) forms keep
+      // one step ahead: with two they spill 2-4 VGPRs.
+      constexpr int kAhead = (QC || NS) ? 1 : kPrefetchFast;
       Frame fa, fb;
       fetch(0, fa);
       if constexpr (EXACT) {
@@ -436,14 +433,25 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
           advance(k, fa);
           fa = fb;
         }
-      } else
-      for (int k = 0; k < a.K; k += 2) {
-        fetch(k + 1, fb);
-        advance(k, fa);
-        fetch(k + 2, fa);
-        if (k + 1 < a.K) advance(k + 1, fb);
+      } else if constexpr (kAhead == 2) {
+        Frame fc;
+        fetch(1, fb);
+        for (int k = 0; k < a.K; k += 3) {
+          fetch(k + 2, fc);
+          advance(k, fa);
+          fetch(k + 3, fa);
+          if (k + 1 < a.K) advance(k + 1, fb);
+          fetch(k + 4, fb);
+          if (k + 2 < a.K) advance(k + 2, fc);
+        }
+      } else {
+        for (int k = 0; k < a.K; k += 2) {
+          fetch(k + 1, fb);
+          advance(k, fa);
+          fetch(k + 2, fa);
+          if (k + 1 < a.K) advance(k + 1, fb);
+        }
       }
-#endif
       if (a.io_in) {  // tfg_update: the frame keeps the inputs, outputs go to the host block
         const int fidx = uni[0].frame, hidx = uni[0].hist;
         R* __restrict__ fr = const_cast<R*>(forc) + (int64_t)fidx * kNumForc * n_pad;
