@@ -25,4 +25,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "calibration $c rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
 done
-python3 scripts/pmc_profile.py $OUT ${PMC_PROFILE:-$OUT/profile.json} 8192 8192 128 67108864 8
+python3 scripts/pmc_profile.py $OUT ${PMC_PROFILE:-$OUT/profile.json} ${PMC_SHAPE:-8192 8192 128} 67108864 8
