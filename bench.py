@@ -81,10 +81,15 @@ FUSE_FALLBACK = 96  # if a device cannot hold FUSE_BIG output slots (main())
 STEP_QUANTUM = 384  # timed steps are a multiple of every depth: the same total work at every N
 
 
-def auto_fuse(cells: int) -> int:
+def auto_fuse(cells: int, elem: int = 4) -> int:
+    """Launch depth by shard size for an engine whose outputs are `elem` bytes
+    (the fp64 engine's history slots are twice the fp32 ones, so half as many
+    fit the same ~210 GB: 192 steps at 4096^2)."""
     if cells > FUSE_SPLIT_CELLS:
-        return FUSE_BIG
-    return FUSE_MID if cells > FUSE_SMALL_CELLS else FUSE_SMALL
+        k = FUSE_BIG
+    else:
+        k = FUSE_MID if cells > FUSE_SMALL_CELLS else FUSE_SMALL
+    return k * 4 // elem
 
 
 def warmup_steps(requested: int, fuse: int) -> int:
@@ -380,7 +385,7 @@ def main():
     ny_global, row0, rows = plan["ny_global"], plan["row0"], plan["rows"]
     fuse_explicit = args.fuse > 0
     if not fuse_explicit:  # by the largest shard, so every rank fuses alike
-        args.fuse = auto_fuse(plan["rows_max"] * args.nx)
+        args.fuse = auto_fuse(plan["rows_max"] * args.nx, 8 if args.engine == "float64" else 4)
     cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
     n_catch = args.catchments + 1 if args.catchments > 0 else 1
     depth_note = None

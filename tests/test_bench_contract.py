@@ -50,6 +50,9 @@ def test_driver_command_times_the_same_work_at_every_n(world, fuse):
     assert bench.timed_steps(48, 24, explicit=True) == 144  # an explicit --fuse: >= 6 launches of it
     # the driver's --warmup 5 still warms one whole launch of the timed depth
     assert bench.warmup_steps(args.warmup, k) == k and bench.warmup_steps(400, k) == 400
+    # the fp64 engine's history slots are twice as large: half the depth, the same timed steps
+    k64 = bench.auto_fuse(plan["rows_max"] * args.nx, 8)
+    assert k64 * 2 == k and bench.timed_steps(args.steps, k64, explicit=False) == 2304
 
 
 def test_weak_scaling_stays_behind_its_flag():
