@@ -33,10 +33,10 @@ constexpr int kBlock = TFG_BLOCK;  // threads per workgroup
 #endif
 constexpr int kCellsPerThread = TFG_CELLS_PER_THREAD;  // adjacent cells per lane
 #ifndef TFG_PREFETCH_DEPTH
-#define TFG_PREFETCH_DEPTH 2  // time steps of forcing requested ahead by the fast engine (1 or 2)
+#define TFG_PREFETCH_DEPTH 2  // time steps of forcing requested ahead by the fast engine (1, 2; 3 to measure)
 #endif
 constexpr int kPrefetchFast = TFG_PREFETCH_DEPTH;
-static_assert(kPrefetchFast == 1 || kPrefetchFast == 2, "TFG_PREFETCH_DEPTH is 1 or 2");
+static_assert(kPrefetchFast >= 1 && kPrefetchFast <= 3, "TFG_PREFETCH_DEPTH is 1, 2 or 3");
 constexpr int kWaves = kBlock / 64;
 constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
 constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
@@ -432,6 +432,20 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
           fetch(k + 1, fb);
           advance(k, fa);
           fa = fb;
+        }
+      } else if constexpr (kAhead == 3) {  // measurement variant (TFG_PREFETCH_DEPTH=3)
+        Frame fc, fd;
+        fetch(1, fb);
+        fetch(2, fc);
+        for (int k = 0; k < a.K; k += 4) {
+          fetch(k + 3, fd);
+          advance(k, fa);
+          fetch(k + 4, fa);
+          if (k + 1 < a.K) advance(k + 1, fb);
+          fetch(k + 5, fb);
+          if (k + 2 < a.K) advance(k + 2, fc);
+          fetch(k + 6, fc);
+          if (k + 3 < a.K) advance(k + 3, fd);
         }
       } else if constexpr (kAhead == 2) {
         Frame fc;
