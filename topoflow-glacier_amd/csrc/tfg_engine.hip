@@ -1036,12 +1036,15 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   if (hipSetDevice(device) != hipSuccess) { h->err = "hipSetDevice failed"; return bail(TFG_ERR_HIP); }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) { h->err = "hipGetDeviceProperties failed"; return bail(TFG_ERR_HIP); }
-  // 128 workgroups per CU: each thread walks ~8 cells at 8192^2.  Freshly
+  // 512 workgroups per CU: each thread walks ~2 cells at 8192^2.  Freshly
   // dispatched workgroups start their per-cell state loads at staggered times,
   // which hides the latency bubble at the start of every cell; measured
-  // +9 % over 8 per CU (broad optimum 64-512 per CU).  The per-workgroup
-  // diagnostic slab is kept under 64 MiB for large catchment counts.
-  h->max_blocks = std::max(256, prop.multiProcessorCount * 128);
+  // +9 % for 128 per CU over 8 (round 1), and with the two-step prefetch
+  // +0.6 % for 512 over 128 at 8192^2, +0.6 % on the 4096 x 8192 shard, even
+  // at 4096^2 (where the chunk count caps it at 256 per CU; DESIGN.md
+  // section 5).  The per-workgroup diagnostic slab is kept under 64 MiB for
+  // large catchment counts.
+  h->max_blocks = std::max(256, prop.multiProcessorCount * 512);
   h->max_blocks = (int)std::max<int64_t>(256, std::min<int64_t>(h->max_blocks, (64ll << 20) / ((int64_t)n_catch * 6 * 8)));
   // a power of two: with many catchments a slab-capped odd count (31775 at 44
   // catchments) measured 10 % slower than 32768 or 16384 (A/B, same box)
