@@ -270,6 +270,9 @@ def test_bmi_grid_topology_of_the_raster():
     for k in range(4):  # edge k of a face joins its nodes k and k + 1
         a, b = fn[:, k], fn[:, (k + 1) % 4]
         assert all(sorted(en[e]) == sorted((i, j)) for e, i, j in zip(fe[:, k], a, b))
+    m.cfg = SimpleNamespace(da=0.25, dx=30.0, dy=40.0)  # the lateral terms' spacing when configured
+    np.testing.assert_array_equal(m.get_grid_spacing(0, np.zeros(2)), [40.0, 30.0])
+    np.testing.assert_array_equal(m.get_grid_x(0, np.zeros(nx)), [0, 30, 60, 90])
 
 
 # ----------------------------------------------------------------- synthetic

@@ -589,8 +589,14 @@ class BmiTopoflowGlacier(BmiBase):
         return shape
 
     def get_grid_spacing(self, grid: int, spacing):
-        d = float(np.sqrt(self.cfg.da) * 1000.0)
-        spacing[:] = (d, d)
+        # (dy, dx) [m] in shape order: the configured spacing of the lateral
+        # terms when given, otherwise square cells of area `da` [km2]
+        dx, dy = getattr(self.cfg, "dx", None), getattr(self.cfg, "dy", None)
+        if dx is not None and dy is not None:
+            spacing[:] = (float(dy), float(dx))
+        else:
+            d = float(np.sqrt(self.cfg.da) * 1000.0)
+            spacing[:] = (d, d)
         return spacing
 
     def get_grid_origin(self, grid: int, origin):
