@@ -868,13 +868,15 @@ struct MeltF {
   double h_swe, h_iwe, Eccs, Ecci;
   float SM, IM, Erem_s, IM_int;  // outputs; terms of the SM and IM integrals (:1486, :1493)
 };
-template <bool NS>
-__device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, float P_snow, float RH, float T_air,
+template <bool NS, class QS>
+__device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P_snow, float RH, float T_air,
                                            double h_swe0, double h_iwe0, double Eccs0, double Ecci0,
                                            double h_ice_prev) {
   MeltF m;
   const double previous_swe = h_swe0;
-  const double E_in = (double)(Q_sum * p.f_dt);
+  double E_in;
+  if constexpr (sizeof(QS) == 8) E_in = Q_sum * p.dt3600;  // an fp64 flux sum (TFG_QSUM_F64)
+  else E_in = (double)(Q_sum * p.f_dt);
   // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
   const double E_rem_s = dmax<NS>(E_in - Eccs0, 0.0);
   m.Erem_s = (float)E_rem_s;
@@ -915,8 +917,8 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, floa
   m.IM = (float)IM;
   return m;
 }
-template <bool NS>
-__device__ __forceinline__ void melt_fast(const DevParams& p, float Q_sum, float P_snow, float P_rain, float RH,
+template <bool NS, class QS>
+__device__ __forceinline__ void melt_fast(const DevParams& p, QS Q_sum, float P_snow, float P_rain, float RH,
                                           float T_air, CellState& st, CellOutF& o, DiagF& d) {
   const MeltF m = melt_core<NS>(p, Q_sum, P_snow, RH, T_air, st.h_swe, st.h_iwe, st.Eccs, st.Ecci, st.h_ice);
   d.Erem_s += m.Erem_s;
@@ -1076,12 +1078,20 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air, ta2 * ta2, -(ts2 * ts2));
+#ifndef TFG_QSUM_F64
+#define TFG_QSUM_F64 0
+#endif
+#if TFG_QSUM_F64  // the flux sum and E_in in fp64 (measurement switch)
+  double Q_sum = (((double)Qn_SW + (double)Qn_LW) + (double)Qh) + (double)Qe;
+  if constexpr (QC) Q_sum = Q_sum + (double)qc;  // :1314, Qc last (Qa = 0)
+#else
   float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
   if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
+#endif
 
   melt_fast<NS>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
 #if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
-  const float dbg[13] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
+  const float dbg[13] = {(float)Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
   o.RH = dbg[TFG_DEBUG_TERM];
 #endif
 }
