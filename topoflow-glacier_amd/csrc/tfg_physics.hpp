@@ -875,7 +875,7 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P
   MeltF m;
   const double previous_swe = h_swe0;
   double E_in;
-  if constexpr (sizeof(QS) == 8) E_in = Q_sum * p.dt3600;  // an fp64 flux sum (TFG_QSUM_F64)
+  if constexpr (sizeof(QS) == 8) E_in = Q_sum * p.dt;  // an fp64 flux sum (TFG_QSUM_F64); dt in hours, as the reference (:1364)
   else E_in = (double)(Q_sum * p.f_dt);
   // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
   const double E_rem_s = dmax<NS>(E_in - Eccs0, 0.0);
