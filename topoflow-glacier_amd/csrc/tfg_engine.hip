@@ -1042,10 +1042,11 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // +9 % for 128 per CU over 8 (round 1), and with the two-step prefetch
   // +0.6 % for 512 over 128 at 8192^2, +0.6 % on the 4096 x 8192 shard, even
   // at 4096^2 (where the chunk count caps it at 256 per CU; DESIGN.md
-  // section 5).  The per-workgroup diagnostic slab is kept under 64 MiB for
-  // large catchment counts.
+  // section 5).  The per-workgroup diagnostic slab is kept under 256 MiB for
+  // large catchment counts: 65536 workgroups at config 5's 43 catchments
+  // (135 MB), +1.2 % on its slab against the 16384 a 64 MiB cap gave.
   h->max_blocks = std::max(256, prop.multiProcessorCount * 512);
-  h->max_blocks = (int)std::max<int64_t>(256, std::min<int64_t>(h->max_blocks, (64ll << 20) / ((int64_t)n_catch * 6 * 8)));
+  h->max_blocks = (int)std::max<int64_t>(256, std::min<int64_t>(h->max_blocks, (256ll << 20) / ((int64_t)n_catch * 6 * 8)));
   // a power of two: with many catchments a slab-capped odd count (31775 at 44
   // catchments) measured 10 % slower than 32768 or 16384 (A/B, same box)
   while (h->max_blocks & (h->max_blocks - 1)) h->max_blocks &= h->max_blocks - 1;
