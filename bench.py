@@ -13,7 +13,7 @@ Workload (N=1): 8192 x 8192 synthetic grid, hourly forcing cycling through 24
 HBM-resident frames, fp32 engine (fp64 state), 128 steps per launch (HBM
 footprint ~266 GB of the 288 GB: 24 forcing frames 32 GB, 128 output slots
 206 GB, 72-slot snowfall window 19 GB, state and geometry 9 GB).  Shards of
-2^25 cells or fewer fuse 192 steps per launch (N = 2), 2^24 or fewer 384
+2^25 cells or fewer fuse 256 steps per launch (N = 2), 2^24 or fewer 384
 (N >= 4; auto_fuse).
 
 --gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
@@ -71,20 +71,21 @@ MIN_LAUNCHES = 6
 # auto launch depth by shard size, as deep as ~210 GB of output slots allow
 # (hist_depth = launch depth): 128 steps above 2^25 cells (the 8192^2 grid: the
 # 128 slots take 206 GB, the whole footprint 266 GB; 96-step launches ran 1.0 %
-# slower on the same box, profiles/r3q_fuse128.log), 192 above 2^24 (4096 x 8192,
-# N = 2: 154 GB), 384 at 2^24 and below (N >= 4: a deeper launch amortises the
-# per-launch cost; 1024 x 8192 with the plane skew 112.6-113.6 -> 115.2-115.7 G
-# cell-updates/s from 192 to 384, profiles/r3ab_slab_k.log)
-FUSE_BIG, FUSE_MID, FUSE_SMALL = 128, 192, 384
+# slower on the same box, profiles/r3q_fuse128.log), 256 above 2^24 (4096 x 8192,
+# N = 2: 206 GB; 121.0-121.4 -> 121.6-121.9 G cell-updates/s from 192 to 256,
+# profiles/r3bn_depth_n2_shard.jsonl), 384 at 2^24 and below (N >= 4: a deeper
+# launch amortises the per-launch cost; 1024 x 8192 with the plane skew
+# 112.6-113.6 -> 115.2-115.7 G cell-updates/s from 192 to 384, profiles/r3ab_slab_k.log)
+FUSE_BIG, FUSE_MID, FUSE_SMALL = 128, 256, 384
 FUSE_SPLIT_CELLS, FUSE_SMALL_CELLS = 1 << 25, 1 << 24
 FUSE_FALLBACK = 96  # if a device cannot hold FUSE_BIG output slots (main())
-STEP_QUANTUM = 384  # timed steps are a multiple of every depth: the same total work at every N
+STEP_QUANTUM = 768  # timed steps are a multiple of every depth: the same total work at every N
 
 
 def auto_fuse(cells: int, elem: int = 4) -> int:
     """Launch depth by shard size for an engine whose outputs are `elem` bytes
     (the fp64 engine's history slots are twice the fp32 ones, so half as many
-    fit the same ~210 GB: 192 steps at 4096^2)."""
+    fit the same ~210 GB: 192 steps at 4096^2, 128 at 4096 x 8192)."""
     if cells > FUSE_SPLIT_CELLS:
         k = FUSE_BIG
     else:
@@ -102,7 +103,7 @@ def timed_steps(requested: int, fuse: int, explicit: bool) -> int:
     """Whole launches covering `requested`, at least MIN_LAUNCHES of them.  With
     the automatic depth the count is a multiple of STEP_QUANTUM covering at
     least MIN_LAUNCHES launches of the deepest automatic depth, so N = 1
-    (128-step launches), N = 2 (192) and N >= 4 (384) time the same number of
+    (128-step launches), N = 2 (256) and N >= 4 (384) time the same number of
     steps of the same grid."""
     if explicit:
         return max(MIN_LAUNCHES, -(-requested // fuse)) * fuse

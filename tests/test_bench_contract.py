@@ -37,10 +37,10 @@ def test_default_shard_plan_is_config4_strong_scaling(world):
     assert plans[0]["scaling"] == "strong"  # one label for the driver's whole N = 1, 2, 4, 8 series
 
 
-@pytest.mark.parametrize("world,fuse", [(1, 128), (2, 192), (4, 384), (8, 384)])
+@pytest.mark.parametrize("world,fuse", [(1, 128), (2, 256), (4, 384), (8, 384)])
 def test_driver_command_times_the_same_work_at_every_n(world, fuse):
     """`--steps 20`: whole launches, >= 6, and the same 2304 steps at every N
-    (128-step launches for the whole 8192^2 grid, 192 for 4096 x 8192, 384 for
+    (128-step launches for the whole 8192^2 grid, 256 for 4096 x 8192, 384 for
     the smaller slabs)."""
     bench, args = _args("--gpus", str(world), "--steps", "20", "--warmup", "5")
     plan = bench.shard_plan(args, world, 0)
