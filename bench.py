@@ -51,17 +51,33 @@ sys.path[:0] = [str(ROOT / "topoflow-glacier_amd"), str(ROOT)]
 
 METRIC = "cell-updates/sec (nx·ny·steps) on 8192² fp32 grid; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# algorithmic bytes per cell (DESIGN.md "Bytes per cell-update")
-BYTES_PER_STEP = 20 + 4 + 4 + 24  # forcing 5xf32, window slot in+out, 6 outputs f32
-BYTES_PER_LAUNCH = 20 + (6 * 8 + 8) * 2  # solar geometry 5xf32; state 6xf64 + window total i64, in and out
+HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
+FORCING = ("P", "T_air", "Hum_sp", "P_air", "uz")
 
 
-def launch_bytes_per_cell(fuse: int) -> int:
-    """Algorithmic HBM bytes per cell of one fused launch:
-    52 per step + 132 per launch.  (Keeping the window slots that a launch
-    reads back itself in LDS would save 8 B per such step, but reserving the
-    LDS cost 8 % of throughput on its own: DESIGN.md section 5.)"""
-    return BYTES_PER_STEP * fuse + BYTES_PER_LAUNCH
+def bytes_model(elem: int = 4, catchments: bool = False, qc: bool = False) -> tuple[int, int]:
+    """Algorithmic HBM bytes per cell of k_fused, as
+    (per step, per launch), for an engine whose forcing frames, output slots
+    and geometry are `elem`-byte values (4: the fp32 engine, 8: the fp64 one):
+      per step:   forcing 5 x elem read, window slot 4 read + 4 written, six
+                  outputs 6 x elem written  (fp32 52 B, fp64 96 B);
+      per launch: geometry (fp32 engine five f32 planes, fp64 engine seven f64
+                  planes), state six f64 + window total i64 read and written,
+                  the catchment id (i32) and Qc (elem) when the variant reads
+                  them  (fp32 132 B, fp64 168 B)."""
+    step = 5 * elem + 4 + 4 + 6 * elem
+    geo = 5 * 4 if elem == 4 else 7 * 8
+    launch = geo + 2 * (6 * 8 + 8) + (4 if catchments else 0) + (elem if qc else 0)
+    return step, launch
+
+
+def launch_bytes_per_cell(fuse: int, elem: int = 4, catchments: bool = False, qc: bool = False) -> int:
+    """Algorithmic HBM bytes per cell of one fused launch of `fuse` steps:
+    fp32 engine 52 per step + 132 per launch, fp64 engine 96 + 168.  (Keeping
+    the window slots that a launch reads back itself in LDS would save 8 B per
+    such step, but reserving the LDS cost 8 % of throughput on its own: HISTORY.md.)"""
+    step, launch = bytes_model(elem, catchments, qc)
+    return step * fuse + launch
 
 MIN_LAUNCHES = 6
 # Why 6: the first launch after the barrier that opens the timed region runs
@@ -78,7 +94,6 @@ MIN_LAUNCHES = 6
 # 112.6-113.6 -> 115.2-115.7 G cell-updates/s from 192 to 384, profiles/r3ab_slab_k.log)
 FUSE_BIG, FUSE_MID, FUSE_SMALL = 128, 256, 384
 FUSE_SPLIT_CELLS, FUSE_SMALL_CELLS = 1 << 25, 1 << 24
-FUSE_FALLBACK = 96  # if a device cannot hold FUSE_BIG output slots (main())
 STEP_QUANTUM = 768  # timed steps are a multiple of every depth: the same total work at every N
 
 
@@ -91,6 +106,43 @@ def auto_fuse(cells: int, elem: int = 4) -> int:
     else:
         k = FUSE_MID if cells > FUSE_SMALL_CELLS else FUSE_SMALL
     return k * 4 // elem
+
+
+DEVICE_BYTES_BUDGET = 280e9  # of an MI355X's 288 GB HBM: the rest for the runtime and torch
+DEPTH_LADDER = (384, 256, 192, 128, 96)  # automatic depths and fallbacks: each divides STEP_QUANTUM
+
+
+def device_footprint(cells: int, frames: int, hist_depth: int, ring_len: int, n_catch: int = 1, elem: int = 4,
+                     catchments: bool = False, cus: int = 256) -> int:
+    """Device bytes of one shard's handle, as tfg_create allocates them
+    (csrc/tfg_engine.hip, tfg_create) plus the catchment raster: per padded
+    cell forcing frames 5 x elem each, static rasters 3 x elem, LW/SW 2 x elem,
+    geometry (fp32 engine 5 x f32 + 2 x f64, fp64 engine 7 x f64), state
+    8 x f64, window total i64, window slots i32 each, output slots 6 x elem
+    each, catchment id i32; plus the per-workgroup diagnostic slab."""
+    n_pad = -(-cells // 64) * 64
+    if n_pad >= 1 << 20:
+        n_pad += 512  # kPlaneSkew
+    geo = 5 * 4 + 2 * 8 if elem == 4 else 7 * 8
+    per = frames * 5 * elem + 3 * elem + 2 * elem + geo + 8 * 8 + 8 + ring_len * 4 + hist_depth * 6 * elem
+    per += 4 if catchments else 0
+    blocks = max(256, min(cus * 512, (256 << 20) // (n_catch * 48)))
+    blocks = 1 << (blocks.bit_length() - 1)
+    blocks = min(blocks, -(-n_pad // 256))
+    return n_pad * per + blocks * n_catch * 48 + n_catch * 48
+
+
+def fit_depth(fuse: int, cells: int, frames: int, ring_len: int, n_catch: int, elem: int, catchments: bool,
+              budget: float = DEVICE_BYTES_BUDGET) -> int:
+    """The automatic depth, or the next shallower one of DEPTH_LADDER while the
+    shard's footprint (history slots = depth) exceeds the device budget."""
+    k = fuse
+    while device_footprint(cells, frames, k, ring_len, n_catch, elem, catchments) > budget:
+        smaller = [d for d in DEPTH_LADDER if d < k]
+        if not smaller:
+            break
+        k = smaller[0]
+    return k
 
 
 def warmup_steps(requested: int, fuse: int) -> int:
@@ -135,9 +187,17 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251001)
     ap.add_argument("--cpu-cells", type=int, default=1048576, help="cells in the C CPU-baseline sample")
     ap.add_argument("--cpu-steps", type=int, default=960, help="steps of the C CPU-baseline sample (~10 s on 16 threads)")
-    ap.add_argument("--parity-steps", type=int, default=96, help="steps of the GPU-vs-oracle spot check")
-    ap.add_argument("--parity-cells", type=int, default=262144,
-                    help="cells of the GPU-vs-oracle spot check (also the numpy one-core sample)")
+    ap.add_argument("--parity-steps", type=int, default=0,
+                    help="steps of the GPU-vs-oracle check after its one-step lead-in launch; 0 = one whole "
+                         "launch of the timed depth (--fuse)")
+    ap.add_argument("--parity-cells", type=int, default=0,
+                    help="cells of each rank's GPU-vs-oracle check (whole rows of its own shard; also the numpy "
+                         "one-core sample at N = 1); 0 = 262144 at N = 1, 65536 per rank at N > 1")
+    ap.add_argument("--no-parity", action="store_true", help="skip the per-rank GPU-vs-oracle check")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in path legs (per-step update() from device inputs, defer_update instances)")
+    ap.add_argument("--dropin-instances", type=int, default=4096,
+                    help="single-catchment BMI models of the defer_update leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie", action="store_true",
                     help="add the PCIe-inclusive (host-fed forcing) leg; off by default so that every k_fused "
@@ -170,13 +230,11 @@ def _floored_rel(g, r):
     return float(np.max(e)), float(np.mean(e > 1e-5))
 
 
-def cpu_baseline(args, run_gpu_sample):
-    """CPU legs on rank 0 at N=1, on the first cells of the shard, same fp32 inputs:
-    (1) the C oracle (oracle/tfg_oracle_c.c, fp64, OpenMP over the process's CPU
-        share) on --cpu-cells x --cpu-steps: the reported cpu_baseline;
-    (2) the numpy oracle (oracle/tfg_oracle.py, fp64, one core) on the first
-        --parity-cells x --parity-steps, reported beside it and used as the
-        reference of a parity spot check of the GPU on those cells and steps."""
+def cpu_baseline(args):
+    """The reported CPU baseline, on rank 0 at N=1: the C oracle
+    (oracle/tfg_oracle_c.c, the fp64 restatement of update(), OpenMP over the
+    process's CPU share) on the first --cpu-cells cells x --cpu-steps steps of
+    the same synthetic workload (the same fp32 inputs as the GPU)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import tfg_oracle as O
     import tfg_oracle_c as OC
@@ -184,70 +242,165 @@ def cpu_baseline(args, run_gpu_sample):
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
     n = min(args.cpu_cells, args.nx * args.ny)
-    steps = max(args.cpu_steps, args.parity_steps)
+    steps = args.cpu_steps
     syn = synthetic_cells(args.seed, np.arange(n), diurnal_table(args.frames))
-    frames = np.arange(steps) % args.frames
-    static = dict(elev=syn["elev"], slope=syn["slope"], aspect=syn["aspect"], h0_snow=syn["h_snow"],
-                  h0_ice=syn["h_ice"], h0_swe=syn["h_swe"], h0_iwe=syn["h_iwe"])
-    static = {k: np.asarray(v, dtype=np.float64) for k, v in static.items()}
+    static = _static_of(syn)
     cfg = dict(BASE_CFG, dt=args.dt)
-    clock = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
-    # (1) C oracle, all threads of this process's share
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
     threads = _cpu_threads()
-    forcing = {k: np.ascontiguousarray(syn[k], dtype=np.float64) for k in ("P", "T_air", "Hum_sp", "P_air", "uz")}
+    forcing = {k: np.ascontiguousarray(syn[k], dtype=np.float64) for k in FORCING}
     t0 = time.perf_counter()
-    out, _ = OC.run_oracle_c(cfg, static, forcing, args.cpu_steps, clock=(clock[0][:args.cpu_steps], clock[3][:args.cpu_steps]),
-                             frames=frames[:args.cpu_steps], hist=False, nthreads=threads)
+    OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=np.arange(steps) % args.frames, hist=False,
+                    nthreads=threads)
     t_c = time.perf_counter() - t0
-    cpu = {"value": n * args.cpu_steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
-           "sample": f"oracle/tfg_oracle_c.c (C fp64 restatement of update(), OpenMP, {threads} threads) on the "
-                     f"first {n} cells x {args.cpu_steps} hourly steps of the same synthetic workload ({t_c:.1f} s)"}
-    # (2) the parity spot check and the one-core numpy leg share one numpy run:
-    # the numpy oracle (bit-identical to the reference on every golden fixture)
-    # over the first pn cells x ps steps is both the reference the GPU is checked
-    # against and the single-core CPU sample.
-    from tests.harness import flip_rule, melt_out_flips, valid_mask
+    return {"value": n * steps / t_c, "unit": "cell-updates/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/tfg_oracle_c.c (C fp64 restatement of update(), OpenMP, {threads} threads) on the "
+                      f"first {n} cells x {steps} {args.dt:g} h steps of the same synthetic workload ({t_c:.1f} s)"}
 
-    pn = min(args.parity_cells, n)
-    ps = args.parity_steps
-    fnp = {k: v[frames[:ps], :pn] for k, v in forcing.items()}
-    snp = {k: v[:pn] for k, v in static.items()}
+
+def _static_of(syn: dict) -> dict:
+    return {k: np.asarray(syn[s], dtype=np.float64) for k, s in (
+        ("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"), ("h0_snow", "h_snow"), ("h0_ice", "h_ice"),
+        ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
+
+
+def parity_plan(args, plan: dict, world: int) -> dict:
+    """The cells and launches of a rank's parity check: whole rows at the top of
+    its OWN shard (global rows row0 .. row0 + rows - 1), and a one-step lead-in
+    launch (the k_fused instance that reads the initial depths) followed by one
+    whole launch of the timed depth, so that the timed kernel instance runs at
+    the timed launch length (at K = 128 the three-register-set step loop ends in
+    its two-step tail)."""
+    want = args.parity_cells or (262144 if world == 1 else 65536)
+    rows = max(1, min(plan["rows"], want // args.nx))
+    k = args.parity_steps or args.fuse
+    return {"row0": plan["row0"], "rows": rows, "cells": rows * args.nx, "launch_steps": [1, k], "steps": 1 + k}
+
+
+def sample_parity(args, plan: dict, world: int, rank: int, local: int, threads: int):
+    """This rank's GPU-vs-oracle check, outside the timed region (every rank,
+    at every N): the engine (same variant as the timed one: engine type, dt,
+    catchments, launch depth) on the first rows of this rank's shard, against
+    the numpy oracle (oracle/tfg_oracle.py, fp64, bit-exact to the reference
+    fixtures) on the host mirror of the same synthetic fp32 inputs, every
+    output at every step.  Cells whose trajectories part at a melt-out residual
+    are compared up to the flip and counted, held to the fp64 baseline of the
+    same cells and steps (the C oracle against the numpy oracle;
+    tests/harness.py flip_rule).  With catchments, the engine's per-catchment
+    precipitation integrals and P_max are checked against bincounts of the
+    forcing, and its melt integrals reported against the oracle's.
+
+    Returns (parity dict, the numpy run's single-core rate as a CPU leg)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import tfg_oracle as O
+    import tfg_oracle_c as OC
+
+    from tests.harness import flip_rule, melt_out_flips, valid_mask
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+    from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
+
+    pp = parity_plan(args, plan, world)
+    rows, nx, row0, steps = pp["rows"], args.nx, pp["row0"], pp["steps"]
+    n = pp["cells"]
+    n_catch = args.catchments + 1 if args.catchments > 0 else 1
+    cid = (catchment_blocks(row0, rows, plan["ny_global"], nx, args.catchments) if args.catchments
+           else np.zeros(n, np.int32))
+    # (1) the GPU: the same engine variant as the timed one
+    scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=nx, dt=args.dt))
+    e = GlacierEngine(scfg, rows, nx, engine=args.engine, device=local, n_frames=args.frames, hist_depth=steps,
+                      fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+    try:
+        e.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=nx)
+        if args.catchments:
+            e.set_field("catch_id", cid)
+        for k in pp["launch_steps"]:
+            e.run(k)
+        e.sync()
+        gpu = {v: np.stack([e.get_field(v, index=j) for j in range(steps)]) for v in HIST}
+        diag = e.diagnostics()
+        ns = e.nan_safe_launches() if args.engine == "float32" else 0
+    finally:
+        e.close()
+    # (2) the numpy oracle on the host mirror of the same inputs (global cell indices)
+    cells = ((row0 + np.arange(rows))[:, None] * nx + np.arange(nx)[None, :]).reshape(-1)
+    syn = synthetic_cells(args.seed, cells, diurnal_table(args.frames))
+    static = _static_of(syn)
+    cfg = dict(BASE_CFG, dt=args.dt)
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
+    frames = np.arange(steps) % args.frames
+    forcing = {k: np.ascontiguousarray(syn[k], dtype=np.float64) for k in FORCING}
+    ref = {v: np.empty((steps, n)) for v in HIST}
     t0 = time.perf_counter()
-    ref, _ = O.run_oracle(cfg, snp, fnp, ps, clock=(clock[0], clock[3]))
+    m = O.OracleGrid(cfg, **static)
+    for k in range(steps):
+        r = m.step(*(forcing[v][frames[k]] for v in FORCING), jd[k], tsn[k])
+        for v in HIST:
+            ref[v][k] = r[v]
     t_np = time.perf_counter() - t0
-    numpy_leg = {"value": pn * ps / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
-                 "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on the first {pn} cells x "
-                           f"{ps} steps ({t_np:.1f} s)"}
-    parity = None
-    gpu = run_gpu_sample(pn, ps)
-    if gpu is not None:
-        # Every step of the first pn cells.  Cells whose trajectories part at a
-        # melt-out residual (DESIGN.md "Melt-out flips") are compared up to the
-        # flip and counted; the count is held to the fp64 baseline of the same
-        # cells and steps: the C oracle against the numpy oracle, two fp64
-        # restatements that differ only in their libm (tests/harness.py flip_rule).
-        names = sorted(gpu)
-        ref = {k: ref[k] for k in names}
-        c64, _ = OC.run_oracle_c(cfg, snp, {k: np.ascontiguousarray(v[:, :pn]) for k, v in forcing.items()}, ps,
-                                 clock=(clock[0][:ps], clock[3][:ps]), frames=frames[:ps], hist=True, nthreads=threads)
-        flip64, genuine64 = melt_out_flips({k: c64[k] for k in names}, ref)
-        flip, genuine = melt_out_flips(gpu, ref)
-        ok = valid_mask(flip, ps)
-        err = max(_floored_rel(g[ok], ref[k][ok])[0] for k, g in gpu.items())
-        pure = {}  # the fraction of compared values above pure-relative 1e-5
-        for k, g in gpu.items():
-            gv, rv = g[ok].astype(np.float64), ref[k][ok]
-            with np.errstate(divide="ignore", invalid="ignore"):
-                rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
-            pure[k] = float(np.mean(rel > 1e-5))
-        rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
-        parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "cells": pn, "steps": ps,
-                  "outputs": names, "max_floored_rel": err, "tolerance": 1e-5, "frac_above_pure_rel_1e-5": pure,
-                  "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"],
-                  "flip_ratio": rule["ratio"], "flip_budget": rule["budget"], "flip_rule": rule["rule"],
-                  "genuine_mismatches": len(genuine), "fp64_baseline_genuine_mismatches": len(genuine64),
-                  "ok": bool(err <= 1e-5 and not genuine and rule["ok"])}
-    return cpu, numpy_leg, parity
+    numpy_leg = {"value": n * steps / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
+                 "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on {n} cells x {steps} steps "
+                           f"({t_np:.1f} s), the reference of the parity check"}
+    c64, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=frames, hist=True, nthreads=threads)
+    flip64, genuine64 = melt_out_flips({v: c64[v] for v in HIST}, ref)
+    flip, genuine = melt_out_flips(gpu, ref)
+    ok = valid_mask(flip, steps)
+    tol = 1e-5 if args.engine == "float32" else 1e-10
+    by_out = {v: _floored_rel(gpu[v][ok], ref[v][ok])[0] for v in HIST}
+    err = max(by_out.values())
+    pure = {}  # SURVEY 8(d): the fraction of compared values above pure-relative 1e-5
+    for v in HIST:
+        gv, rv = gpu[v][ok], ref[v][ok]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
+        pure[v] = float(np.mean(rel > 1e-5))
+    rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
+    # the mass-balance integrals of the same launches (:558-624, :1482-1494), per catchment
+    kc = max(args.catchments, 1)
+    da_dt = BASE_CFG["da"] * 1e6 * args.dt
+    Pk = forcing["P"][frames]
+    rain = forcing["T_air"][frames] > BASE_CFG["T_rain_snow"]
+    want = np.stack([np.bincount(cid, weights=w, minlength=kc)[:kc] * da_dt
+                     for w in (Pk.sum(0), np.where(rain, Pk, 0.0).sum(0), np.where(rain, 0.0, Pk).sum(0))], axis=1)
+    pmax = np.array([Pk[:, cid == c].max() if np.any(cid == c) else 0.0 for c in range(kc)])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        p_err = float(np.max(np.where(want != 0, np.abs(diag[:kc, :3] - want) / np.abs(want), np.abs(diag[:kc, :3]))))
+    melt = {}
+    for col, v in ((3, "SM"), (4, "IM")):
+        w = np.bincount(cid, weights=np.broadcast_to(getattr(m, "cell_vol_" + v), (n,)), minlength=kc)[:kc]
+        melt[f"vol_{v}_max_rel"] = float(np.max(np.abs(diag[:kc, col] - w)) / max(float(np.max(np.abs(w))), 1e-300))
+    mass = {"catchments": kc, "vol_P_PR_PS_max_rel": p_err, "vol_P_PR_PS_tolerance": 1e-6,
+            "P_max_exact": bool(np.array_equal(diag[:kc, 5], pmax)), **melt,
+            "note": "vol_SM / vol_IM reported, not gated: a melt-out flip moves a cell's melt by a step"}
+    engine_desc = ("k_fused<float, READ_DEPTHS=false, CATCH=%s, QC=false, clean form>" % ("true" if args.catchments else "false")
+                   if args.engine == "float32" else "k_fused<double, exact, READ_DEPTHS=false>")
+    parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "rank": rank,
+              "global_rows": [row0, row0 + rows - 1], "cells": n, "steps": pp["launch_steps"][1],
+              "lead_in_steps": pp["launch_steps"][0], "steps_compared": steps, "launch_steps": pp["launch_steps"],
+              "timed_kernel_instance": engine_desc + f" in a {pp['launch_steps'][1]}-step launch, after a one-step "
+                                                     f"lead-in launch that reads the initial depths",
+              "nan_safe_launches": ns, "outputs": list(HIST), "max_floored_rel": err,
+              "max_floored_rel_by_output": by_out, "tolerance": tol, "frac_above_pure_rel_1e-5": pure,
+              "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"], "flip_ratio": rule["ratio"],
+              "flip_budget": rule["budget"], "flip_rule": rule["rule"], "genuine_mismatches": len(genuine),
+              "fp64_baseline_genuine_mismatches": len(genuine64), "mass_balance": mass,
+              "ok": bool(err <= tol and not genuine and rule["ok"] and ns == 0 and p_err <= 1e-6
+                         and mass["P_max_exact"])}
+    return parity, numpy_leg
+
+
+def parity_summary(per_rank: list[dict]) -> dict:
+    """The N > 1 line's parity: every rank's own check (ranks[].sample_parity) folded."""
+    ok = [p for p in per_rank if p is not None]
+    if not ok:
+        return None
+    return {"vs": ok[0]["vs"], "ranks_checked": [p["rank"] for p in ok], "cells": sum(p["cells"] for p in ok),
+            "steps": ok[0]["steps"], "steps_compared": ok[0]["steps_compared"],
+            "max_floored_rel": max(p["max_floored_rel"] for p in ok), "tolerance": ok[0]["tolerance"],
+            "melt_out_flips": sum(p["melt_out_flips"] for p in ok),
+            "flips_fp64_baseline": sum(p["flips_fp64_baseline"] for p in ok),
+            "genuine_mismatches": sum(p["genuine_mismatches"] for p in ok),
+            "per_rank": "ranks.ranks[].sample_parity", "ok": all(p["ok"] for p in ok) and len(ok) == len(per_rank)}
 
 
 def shard_plan(args, world: int, rank: int) -> dict:
@@ -353,6 +506,123 @@ def pcie_inclusive(eng, args, torch):
                       f"memory, synchronously, then one fused launch"}
 
 
+def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
+    """The grid path NextGen drives (examples/run_topoflow_glacier.py:64-109,
+    tests/integration_test.py:102-147 of the reference: set the inputs, then
+    update(), every step), with the inputs already on the device: per step
+    one tfg_set_inputs from a device [5][n] f32 block (BMI order P_air, Hum_sp,
+    P, T_air, uz: 20 B read + 20 B written per cell) and one tfg_step of one
+    step (a K = 1 launch: 52 + 132 = 184 B per cell-update).  Beside it the
+    same steps queued: the inputs of `steps` steps set into as many frames,
+    then one fused launch (what a deferred grid update() would do).  Never
+    `value`."""
+    names = ("P_air", "Hum_sp", "P", "T_air", "uz")
+    n = eng.n
+    steps = min(steps, args.frames, args.fuse)
+    blk = torch.empty((5, n), dtype=torch.float32, device=f"cuda:{eng.device}")
+    for i, name in enumerate(names):  # frame 0's values: the physics stays in range
+        eng.get_field_device(name, blk[i], index=0)
+    step_b, launch_b = bytes_model(4)
+    out = {"cells": n, "steps": steps,
+           "protocol": "per step: tfg_set_inputs (device f32 [5][n]) + tfg_step(1); queued: the same inputs into "
+                       f"{steps} frames, then one {steps}-step launch"}
+    for mode in ("per_step", "queued"):
+        ns0 = eng.nan_safe_launches()
+        ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize(eng.device)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        if mode == "per_step":
+            for s in range(steps):
+                eng.set_inputs(blk, index=eng.step_index % args.frames)
+                ev_k[s][0].record(stream)
+                eng.run(1)
+                ev_k[s][1].record(stream)
+        else:
+            for s in range(steps):
+                eng.set_inputs(blk, index=(eng.step_index + s) % args.frames)
+            eng.run(steps)
+        e1.record(stream)
+        torch.cuda.synchronize(eng.device)
+        wall = time.perf_counter() - t0
+        dev_ms = e0.elapsed_time(e1)
+        rec = {"value": n * steps / wall, "unit": "cell-updates/s", "ms_per_step": wall / steps * 1e3,
+               "device_ms_per_step": dev_ms / steps, "nan_safe_launches": eng.nan_safe_launches() - ns0}
+        if mode == "per_step":
+            k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_k]))
+            rec.update({"step_launch_ms": k_ms, "bytes_per_cell_update": step_b + launch_b,
+                        "step_launch_GBps": n * (step_b + launch_b) / (k_ms / 1e3) / 1e9,
+                        "bytes_per_cell_update_with_input_copy": step_b + launch_b + 40})
+            rec["step_launch_frac"] = rec["step_launch_GBps"] / HBM_PEAK_GBS
+        else:
+            rec.update({"bytes_per_cell_update": step_b + launch_b / steps + 40})
+        rec["device_GBps"] = n * rec["bytes_per_cell_update" if mode == "queued" else
+                                     "bytes_per_cell_update_with_input_copy"] / (dev_ms / steps / 1e3) / 1e9
+        rec["frac"] = rec["device_GBps"] / HBM_PEAK_GBS
+        out[mode] = rec
+    del blk
+    return out
+
+
+def dropin_instances_leg(args, local: int, steps: int = 8) -> dict:
+    """NextGen's many-catchment pattern: one single-catchment BMI model per
+    catchment in one process (examples/run_topoflow_glacier.py:64-109 per
+    model), with the additive key defer_update: every model's 7 set_value and
+    update() (queued), then every model's 8 get_value (the first one runs all
+    queued steps: one tfg_update_many call, one k_cell_many launch).  One
+    untimed round first.  Never `value`."""
+    import tempfile
+
+    import yaml
+
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    with tempfile.TemporaryDirectory() as td:
+        cfgf = Path(td) / "cat.yaml"
+        cfgf.write_text(yaml.safe_dump(dict(BASE_CFG, defer_update=True, device=local)))
+        t0 = time.perf_counter()
+        models = []
+        for _ in range(args.dropin_instances):
+            m = BmiTopoflowGlacier()
+            m.initialize(str(cfgf))
+            models.append(m)
+        t_create = time.perf_counter() - t0
+    ins = {"atmosphere_water__liquid_equivalent_precipitation_rate": 1e-7, "land_surface_air__temperature": -2.0,
+           "land_surface_air__pressure": 88000.0, "atmosphere_air_water~vapor__relative_saturation": 0.003,
+           "wind_speed_UV": 3.0, "land_surface_radiation~incoming~longwave__energy_flux": 250.0,
+           "land_surface_radiation~incoming~shortwave__energy_flux": 100.0}
+    vals = {k: np.array([v]) for k, v in ins.items()}
+    outs = models[0].get_output_var_names()
+    buf = np.zeros(1)
+    t_set = t_get = 0.0
+    for r in range(steps + 1):  # round 0 untimed
+        a = time.perf_counter()
+        for m in models:
+            for k, v in vals.items():
+                m.set_value(k, v)
+            m.update()
+        b = time.perf_counter()
+        for m in models:
+            for k in outs:
+                m.get_value(k, buf)
+        c = time.perf_counter()
+        if r:
+            t_set += b - a
+            t_get += c - b
+    ref = models[0].get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0]
+    same = all(m.get_value("land_surface_water__runoff_volume_flux", np.zeros(1))[0] == ref for m in models)
+    for m in models:
+        m.finalize()
+    per = (t_set + t_get) / (len(models) * steps) * 1e6
+    return {"instances": len(models), "steps": steps, "us_per_instance_step": per,
+            "instance_steps_per_s": 1e6 / per, "us_set_and_update": t_set / (len(models) * steps) * 1e6,
+            "us_get_incl_launch": t_get / (len(models) * steps) * 1e6, "create_s": t_create,
+            "all_instances_equal": bool(same),
+            "protocol": "ensemble order: every model's 7 set_value + update() (queued), then every model's "
+                        "8 get_value (the first runs the queued steps in one k_cell_many launch)"}
+
+
 def main():
     args = parse()
     import torch
@@ -385,23 +655,31 @@ def main():
     args.scaling = plan["scaling"]
     ny_global, row0, rows = plan["ny_global"], plan["row0"], plan["rows"]
     fuse_explicit = args.fuse > 0
-    if not fuse_explicit:  # by the largest shard, so every rank fuses alike
-        args.fuse = auto_fuse(plan["rows_max"] * args.nx, 8 if args.engine == "float64" else 4)
     cfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=args.nx, dt=args.dt))
     n_catch = args.catchments + 1 if args.catchments > 0 else 1
+    elem = 8 if args.engine == "float64" else 4
+    ring_len = int(3 * 24 / args.dt)
     depth_note = None
-    try:
-        eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
-                            hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
-    except NativeError as e:
-        # the 128-step history takes 206 GB of the 266 GB footprint at 8192^2: where a
-        # device cannot hold it, the round-2 depth (96 steps, 212 GB) times the same steps
-        if fuse_explicit or args.fuse != FUSE_BIG or "memory" not in str(e).lower():
-            raise
-        depth_note = f"{FUSE_BIG}-step history did not fit ({e}); fused {FUSE_FALLBACK} steps"
-        args.fuse = FUSE_FALLBACK
-        eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
-                            hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+    if not fuse_explicit:  # by the largest shard, so every rank fuses alike
+        auto = auto_fuse(plan["rows_max"] * args.nx, elem)
+        args.fuse = fit_depth(auto, plan["rows_max"] * args.nx, args.frames, ring_len, n_catch, elem,
+                              args.catchments > 0)
+        if args.fuse != auto:
+            depth_note = f"{auto}-step history over the {DEVICE_BYTES_BUDGET / 1e9:.0f} GB budget; fused {args.fuse} steps"
+    while True:
+        try:
+            eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+                                hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+            break
+        except NativeError as e:
+            # a device that cannot hold the history of the automatic depth fuses the
+            # next shallower one (each divides the timed step count)
+            smaller = [d for d in DEPTH_LADDER if d < args.fuse]
+            if fuse_explicit or not smaller or "memory" not in str(e).lower():
+                raise
+            depth_note = f"{args.fuse}-step history did not fit ({e}); fused {smaller[0]} steps"
+            args.fuse = smaller[0]
+            torch.cuda.empty_cache()
     eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
     if args.catchments > 0:
         eng.set_field("catch_id", catchment_blocks(row0, rows, ny_global, args.nx, args.catchments))
@@ -451,9 +729,25 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    cells = rows * args.nx
+    diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
+    bytes_launch = cells * launch_bytes_per_cell(args.fuse, elem, args.catchments > 0, args.conduction)
+    achieved = bytes_launch / (float(launch_ms.mean()) / 1e3) / 1e9
+    # launches of the timed region that ran the fp32 step's NaN-safe form (0: the clean form was timed)
+    ns_timed = (eng.nan_safe_launches() - ns_before) if args.engine == "float32" else None
+    # the host-fed leg, the drop-in legs and the CPU baseline run on rank 0 at N=1 only (BASELINE contract)
+    pcie = pcie_inclusive(eng, args, torch) if world == 1 and args.pcie else None
+    dropin_grid = dropin_grid_leg(eng, args, torch, stream) if world == 1 and not args.no_dropin else None
+    eng.close()
+    torch.cuda.empty_cache()
+    # every rank checks its own shard's first rows against the oracle (outside the timed region)
+    parity = numpy_leg = None
+    if not args.no_parity:
+        parity, numpy_leg = sample_parity(args, plan, world, rank, local, _cpu_threads())
     own = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **device_record(torch, local),
            "row0": row0, "rows": rows, "elapsed_s": elapsed, "launch_ms_mean": float(launch_ms.mean()),
-           "launch_ms_min": float(launch_ms.min()), "launch_ms_max": float(launch_ms.max())}
+           "launch_ms_min": float(launch_ms.min()), "launch_ms_max": float(launch_ms.max()),
+           "sample_parity": parity}
     records = [own]
     if pg:
         records = [None] * dist.get_world_size()
@@ -463,39 +757,19 @@ def main():
     if pg:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    cells = rows * args.nx
     total_cells = ny_global * args.nx if args.scaling == "strong" else cells * world
     value = total_cells * steps / elapsed
-    diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
-
-    mean_launch_s = float(launch_ms.mean()) / 1e3
-    bytes_launch = cells * launch_bytes_per_cell(args.fuse)
-    achieved = bytes_launch / mean_launch_s / 1e9
-    # launches of the timed region that ran the fp32 step's NaN-safe form (0: the clean form was timed)
-    ns_timed = (eng.nan_safe_launches() - ns_before) if args.engine == "float32" else None
-    # the host-fed leg and the CPU baseline run on rank 0 at N=1 only (BASELINE contract)
-    pcie = pcie_inclusive(eng, args, torch) if world == 1 and args.pcie else None
-    eng.close()
 
     result = None
     if rank == 0:
-        cpu = numpy_leg = parity = None
+        cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            def run_gpu_sample(n, steps):
-                # the GPU engine on the CPU sample's cells and steps (a parity spot check)
-                scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=1, nx=n, dt=args.dt))
-                se = GlacierEngine(scfg, 1, n, engine=args.engine, device=local, n_frames=args.frames,
-                                   hist_depth=steps, fuse_steps=args.fuse)
-                try:
-                    se.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=n)
-                    se.run(steps)
-                    se.sync()
-                    return {k: np.stack([se.get_field(k, index=j) for j in range(steps)])
-                            for k in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")}
-                finally:
-                    se.close()
-
-            cpu, numpy_leg, parity = cpu_baseline(args, run_gpu_sample)
+            cpu = cpu_baseline(args)
+        dropin_many = None
+        if world == 1 and not args.no_dropin and args.dropin_instances > 0:
+            dropin_many = dropin_instances_leg(args, local)
+        if world > 1:
+            parity = parity_summary([r["sample_parity"] for r in ranks["ranks"]]) if not args.no_parity else None
         traffic, traffic_source = pmc_traffic(rows, args)
         result = {
             "metric": METRIC,
@@ -549,14 +823,16 @@ def main():
                 "traffic_source": traffic_source,
                 "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
                 "kernel_ms_per_launch": float(launch_ms.mean()),
+                "bytes_model": dict(zip(("per_step", "per_launch"), bytes_model(elem, args.catchments > 0, args.conduction))),
                 "note": None if args.engine == "float32" else (
-                    "the fp64 engine is compute-bound, not HBM-bound: its step issues 1088 VALU instructions per "
-                    "wave and cell-step, 81 % of the vector pipe at 4 waves per SIMD (profiles/r3z_issue_counters.json); "
-                    "frac is its HBM share only"),
+                    "the fp64 engine is issue-bound, not HBM-bound: its step issues 1088-1092 VALU instructions per "
+                    "wave and cell-step (profiles/r3az_issue_counters.json); frac is its HBM share only"),
             },
             "cpu_baseline": cpu,
-            "cpu_baseline_numpy_1core": numpy_leg,
+            "cpu_baseline_numpy_1core": numpy_leg if world == 1 else None,
             "pcie_inclusive": pcie,
+            "dropin_per_step_grid": dropin_grid,
+            "dropin_defer_update_instances": dropin_many,
             "conduction_host_ms_per_update": (float(np.mean(cond_ms)) if cond_ms else None),
             "sample_parity": parity,
             "mass_balance": {k: float(v) for k, v in zip(["vol_P", "vol_PR", "vol_PS", "vol_SM", "vol_IM", "P_max"], diag[0])},

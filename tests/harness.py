@@ -344,6 +344,30 @@ def oracle_synthetic(seed: int, ny: int, nx: int, nsteps: int, n_frames: int = 2
     return {key: np.stack(v) for key, v in out.items()}, m
 
 
+def catchment_diag(syn: dict, m, cid: np.ndarray, nsteps: int, n_frames: int, n_catch: int, cfg: dict) -> np.ndarray:
+    """[n_catch][6] per-catchment vol_P, vol_PR, vol_PS, vol_SM, vol_IM, P_max
+    of an oracle run over synthetic cells (:558-624, :1482-1494 summed per
+    catchment): the precipitation terms binned from the forcing frames the
+    steps read, the melt integrals from the oracle's per-cell contributions."""
+    c = dict(BASE_CFG)
+    c.update(cfg)
+    frames = np.arange(nsteps) % n_frames
+    P = syn["P"][frames].astype(np.float64)
+    rain = syn["T_air"][frames].astype(np.float64) > float(c["T_rain_snow"])
+    f = float(c["da"]) * 1e6 * float(c["dt"])
+    out = np.zeros((n_catch, 6))
+    for col, w in enumerate((P, np.where(rain, P, 0.0), np.where(rain, 0.0, P))):
+        out[:, col] = np.bincount(cid, weights=(w * f).sum(axis=0), minlength=n_catch)
+    n = cid.size
+    out[:, 3] = np.bincount(cid, weights=np.broadcast_to(m.cell_vol_SM, (n,)), minlength=n_catch)
+    out[:, 4] = np.bincount(cid, weights=np.broadcast_to(m.cell_vol_IM, (n,)), minlength=n_catch)
+    pmax = P.max(axis=0)
+    for k in range(n_catch):
+        sel = cid == k
+        out[k, 5] = pmax[sel].max() if sel.any() else 0.0
+    return out
+
+
 def oracle_diag(m) -> np.ndarray:
     """[1][6] diagnostics row of an oracle model (vol_P, PR, PS, SM, IM, P_max)."""
     return np.array([[m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM, m.P_max]], dtype=np.float64)

@@ -36,6 +36,22 @@ def main():
     # the diagnostics all-reduce (sum of columns 0-4, max of column 5) on device tensors
     d = np.arange(18, dtype=np.float64).reshape(3, 6) * 0.25 - 1.0
     res["diag_in"], res["diag_out"] = d, allreduce_diagnostics(d)
+    # config 5's per-catchment mass balance through the same all-reduce: an
+    # engine shard with bench.py's 43-catchment block raster (rows 6144.. of a
+    # 16384-row grid, as rank 3 of 8 holds them), dt = 0.25 h, 96 fused steps
+    import bench
+    from topoflow_glacier.synthetic import diurnal_table
+
+    cny, cnx, crow0 = 64, 512, 6144
+    e = make_engine(dict(BASE_CFG, dt=0.25), cny, cnx, "float32", n_frames=24, hist_depth=96, n_catch=44,
+                    fuse_steps=96, row0=crow0)
+    e.fill_synthetic(20251001, diurnal_table(24), nx_global=cnx)
+    e.set_field("catch_id", bench.catchment_blocks(crow0, cny, 16384, cnx, 43))
+    e.run(192)
+    e.sync()
+    dc = e.diagnostics()
+    e.close()
+    res["catch_diag_in"], res["catch_diag_out"] = dc, allreduce_diagnostics(dc)
     # a batched isend / irecv of a device tensor with this rank itself
     x = torch.arange(64, dtype=torch.float64, device="cuda") * 1.5
     y = torch.full_like(x, -1.0)

@@ -24,7 +24,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain", "flow", "gpu_flow", "cond", "gpu_cond"], required=True)
+    ap.add_argument("--mode", choices=["oracle", "gpu", "halo", "gpu_terrain", "flow", "gpu_flow", "cond", "gpu_cond", "catch"], required=True)
     ap.add_argument("--ny", type=int, required=True)
     ap.add_argument("--nx", type=int, required=True)
     ap.add_argument("--steps", type=int, required=True)
@@ -109,6 +109,24 @@ def main():
         np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, qc=qc)
         if a.mode == "gpu_cond":
             sh.close()
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    if a.mode == "catch":
+        # config 5's per-catchment mass balance over row blocks: bench.py's
+        # 43-catchment block raster of the global grid, dt = 0.25 h (a 288-slot
+        # window), the oracle on this rank's rows, [44][6] per-catchment
+        # integrals combined by allreduce_diagnostics
+        import bench
+        from tests.harness import catchment_diag, oracle_synthetic, synthetic_inputs
+
+        cfg = {"dt": 0.25}
+        ref, m = oracle_synthetic(a.seed, rows, a.nx, a.steps, a.frames, row0=row0, cfg_over=cfg)
+        syn, _ = synthetic_inputs(a.seed, rows, a.nx, a.frames, row0=row0)
+        cid = bench.catchment_blocks(row0, rows, a.ny, a.nx, 43)
+        diag = catchment_diag(syn, m, cid, a.steps, a.frames, 44, cfg)
+        np.savez(Path(a.out) / f"rank{rank}.npz", row0=row0, rows=rows, diag=diag, reduced=allreduce_diagnostics(diag),
+                 cid=cid)
         dist.barrier()
         dist.destroy_process_group()
         return

@@ -55,6 +55,64 @@ def test_driver_command_times_the_same_work_at_every_n(world, fuse):
     assert k64 * 2 == k and bench.timed_steps(args.steps, k64, explicit=False) == 2304
 
 
+def test_byte_model_prices_each_engine_by_its_element_size():
+    """roofline.achieved's algorithmic bytes: the fp32 engine 52 B per step +
+    132 B per launch (53.03 B per cell-update at the bench's 128-step
+    launches), the fp64 engine 96 + 168 (its forcing frames, output slots and
+    geometry are f64: 96.875 B at its automatic 192 steps on 4096^2)."""
+    bench, _ = _args()
+    assert bench.bytes_model(4) == (52, 132) and bench.bytes_model(8) == (96, 168)
+    assert bench.launch_bytes_per_cell(128) / 128 == 53.03125
+    k64 = bench.auto_fuse(4096 * 4096, 8)
+    assert k64 == 192 and bench.launch_bytes_per_cell(k64, 8) / k64 == 96.875
+    # the catchment variant reads the id raster, the conduction variant Qc, once per launch
+    assert bench.bytes_model(4, catchments=True, qc=True) == (52, 132 + 4 + 4)
+
+
+def test_config5_eight_gpu_command_fits_its_shards():
+    """BASELINE config 5 as the driver would run it on 8 GPUs
+    (`--gpus 8 --ny 16384 --nx 16384 --dt 0.25 --catchments 43`): 2048 x 16384
+    cells per rank, the automatic 256-step depth, a 288-slot snowfall window,
+    and a per-rank device footprint (tfg_create's allocations at that depth)
+    within the 280 GB budget, so no rank falls back; the 43 catchments of the
+    block raster all occur, spread over the ranks' rows."""
+    bench, args = _args("--gpus", "8", "--ny", "16384", "--nx", "16384", "--dt", "0.25", "--catchments", "43")
+    plans = [bench.shard_plan(args, 8, r) for r in range(8)]
+    assert all(p["rows"] == 2048 for p in plans) and plans[0]["workload"] == "16384x16384 grid (2048x16384 per GPU)"
+    rows = np.concatenate([np.arange(p["row0"], p["row0"] + p["rows"]) for p in plans])
+    assert np.array_equal(rows, np.arange(16384))
+    cells = 2048 * 16384
+    k = bench.auto_fuse(cells)
+    ring = int(3 * 24 / 0.25)
+    assert k == 256 and ring == 288
+    fp = bench.device_footprint(cells, 24, k, ring, 44, 4, True)
+    assert 250e9 < fp <= bench.DEVICE_BYTES_BUDGET, fp
+    assert bench.fit_depth(k, cells, 24, ring, 44, 4, True) == k
+    steps = bench.timed_steps(20, k, explicit=False)
+    assert steps == 2304 and steps % k == 0
+    # the 8192^2 headline shard at 128 steps: ~266 GB, also within budget
+    assert bench.device_footprint(8192 * 8192, 24, 128, 72, 1) <= bench.DEVICE_BYTES_BUDGET
+    # a depth that would not fit falls back down the ladder (each step count divides 768)
+    assert bench.fit_depth(384, cells, 24, ring, 44, 4, True) == 256
+    assert all(bench.STEP_QUANTUM % d == 0 for d in bench.DEPTH_LADDER)
+    ids = np.unique(np.concatenate([bench.catchment_blocks(p["row0"], p["rows"], 16384, 16384, 43) for p in plans]))
+    assert np.array_equal(ids, np.arange(43))
+    # every rank's parity check covers its own first rows (65536 cells = 4 rows of 16384)
+    pp = [bench.parity_plan(args, p, 8) for p in plans]
+    assert [q["row0"] for q in pp] == [p["row0"] for p in plans] and all(q["cells"] == 65536 for q in pp)
+
+
+def test_parity_check_runs_the_timed_launch_shape():
+    """N = 1: the parity check's GPU run is a one-step lead-in launch (the
+    instance that reads the initial depths) then ONE whole launch of the
+    timed depth (128 steps at 8192^2), on the first 32 rows of the grid."""
+    bench, args = _args("--gpus", "1")
+    args.fuse = bench.auto_fuse(8192 * 8192)
+    plan = bench.shard_plan(args, 1, 0)
+    pp = bench.parity_plan(args, plan, 1)
+    assert pp["launch_steps"] == [1, 128] and pp["steps"] == 129 and pp["cells"] == 262144 and pp["rows"] == 32
+
+
 def test_weak_scaling_stays_behind_its_flag():
     bench, args = _args("--gpus", "4", "--scaling", "weak")
     p = [bench.shard_plan(args, 4, r) for r in range(4)]
@@ -64,8 +122,8 @@ def test_weak_scaling_stays_behind_its_flag():
 @pytest.mark.gpu
 def test_bench_prints_one_json_line_with_the_contract_keys():
     cmd = [sys.executable, str(ROOT / "bench.py"), "--ny", "256", "--nx", "1024", "--steps", "48", "--warmup", "24",
-           "--fuse", "24", "--cpu-cells", "4096", "--cpu-steps", "48", "--parity-cells", "2048", "--parity-steps", "24",
-           "--no-pcie"]
+           "--fuse", "24", "--cpu-cells", "4096", "--cpu-steps", "48", "--parity-cells", "2048",
+           "--dropin-instances", "64"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -88,6 +146,15 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     sp = d["sample_parity"]
     assert sp["genuine_mismatches"] == 0 and sp["max_floored_rel"] <= sp["tolerance"]
     assert sp["ok"] and sp["melt_out_flips"] <= sp["flip_budget"] and "flips_fp64_baseline" in sp
+    # the check runs the timed launch depth after a one-step lead-in, on the clean step form
+    assert sp["steps"] == 24 and sp["launch_steps"] == [1, 24] and sp["steps_compared"] == 25
+    assert sp["cells"] == 2048 and sp["nan_safe_launches"] == 0 and sp["mass_balance"]["P_max_exact"]
+    assert d["ranks"]["ranks"][0]["sample_parity"]["ok"]
+    # the drop-in legs: per-step K = 1 launches from device inputs, and queued steps; defer_update instances
+    g = d["dropin_per_step_grid"]
+    assert g["per_step"]["value"] > 0 and g["queued"]["value"] > 0 and g["per_step"]["bytes_per_cell_update"] == 184
+    mi = d["dropin_defer_update_instances"]
+    assert mi["instances"] == 64 and mi["us_per_instance_step"] > 0 and mi["all_instances_equal"]
     ts = rf["traffic_source"]  # no PMC profile of this shape: traffic is null and says why
     assert rf["traffic"] is None and ts["reason"]
 
@@ -132,3 +199,9 @@ def test_multi_rank_line_is_self_verifying():
     for x in rep["ranks"]:
         assert x["pci_bus_id"] and x["device"] == 0 and x["launch_ms_min"] <= x["launch_ms_mean"] <= x["launch_ms_max"]
     assert rep["n_distinct_gpus"] == 1 and not rep["distinct_gpus"]  # both ranks on the one GPU of the box
+    # every rank checked its OWN rows against the oracle (global row offsets), folded into the line's parity
+    for x in rep["ranks"]:
+        sp = x["sample_parity"]
+        assert sp["ok"] and sp["global_rows"][0] == x["row0"] and sp["genuine_mismatches"] == 0
+        assert sp["steps"] == 24 and sp["launch_steps"] == [1, 24]
+    assert d["sample_parity"]["ok"] and d["sample_parity"]["ranks_checked"] == [0, 1]

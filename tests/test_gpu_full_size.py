@@ -1,8 +1,11 @@
 """Parity at the BASELINE.json GPU configurations' per-GPU sizes.
 
-  * config 4 (the bench): 8192 x 8192, hourly, two 96-step launches (the
-    bench's launch shape: longer than the 72-slot window, so a launch reads
-    back window slots it wrote itself);
+  * config 4 (the bench): 8192 x 8192, hourly, two launches of the bench's
+    automatic depth (bench.auto_fuse: 128 steps).  The first reads the initial
+    depths; the second is the timed kernel instance at the timed launch
+    length, whose step loop (three register sets) ends in its two-step tail
+    (128 = 3 * 42 + 2).  Both are longer than the 72-slot window, so a launch
+    reads back window slots it wrote itself;
   * config 3: 4096 x 4096, hourly, two 24-step launches;
   * config 2: 1024 x 1024, a year of hourly steps (8760) in 120-step launches,
     the oracle's daily outputs on about 2048 sampled cells
@@ -32,6 +35,7 @@ holds at any size:
 import numpy as np
 import pytest
 
+import bench
 from tests.harness import (BASE_CFG, c_oracle_hist, flip_rule, fp64_baseline_flips, make_engine, melt_out_flips,
                            oracle_run, valid_mask)
 
@@ -41,7 +45,8 @@ SEED = 20251001
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
 CONFIGS = {
     # name: (ny, nx, row0, ny_global, dt, steps, fuse, catchments)
-    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 192, 96, 0),  # the bench's launch shape
+    # the bench's launch shape: two launches of its automatic depth at 8192^2
+    "config4_8192sq": (8192, 8192, 0, 8192, 1.0, 2 * bench.auto_fuse(8192 * 8192), bench.auto_fuse(8192 * 8192), 0),
     "config3_4096sq": (4096, 4096, 0, 4096, 1.0, 48, 24, 0),
     "config5_slab_2048x16384_dt0.25_43catch": (2048, 16384, 6144, 16384, 0.25, 384, 96, 43),
     # the largest shard tfg_create accepts (n_pad * 8 < 2^32: fp64 planes at

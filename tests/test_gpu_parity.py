@@ -983,3 +983,56 @@ def test_fp32_form_choice_checks_unknown_data_once():
     for v in sa:
         np.testing.assert_array_equal(sa[v], sb[v], err_msg=v)
     np.testing.assert_array_equal(oa, ob)
+
+
+def test_device_sets_stay_stream_ordered_and_are_checked_lazily():
+    """tfg_set_field from device memory: the plane is marked of
+    unknown finite-data status instead of checked synchronously, so a short
+    launch runs the NaN-safe form and a launch of 8 or more steps checks it
+    first and runs the clean form; a device-set elevation raster holding a NaN
+    is found by that check and sends the launch to the NaN-safe form.  The
+    results equal host-set runs bit for bit."""
+    import ctypes
+
+    import torch
+
+    from topoflow_glacier import _native as nat
+    from topoflow_glacier.synthetic import diurnal_table
+
+    ny, nx, seed = 6, 40, 5
+    runs = []
+    for device in (False, True):
+        e = make_engine(BASE_CFG, ny, nx, "float32", n_frames=24, hist_depth=40, fuse_steps=40)
+        try:
+            e.fill_synthetic(seed, diurnal_table(24))
+            t0 = e.get_field("T_air", index=0, dtype=np.float32)
+            if device:
+                d = torch.as_tensor(t0, device="cuda:0")
+                torch.cuda.synchronize()
+                e._chk(e.lib.tfg_set_field(e.h, nat.FIELD["T_air"], 0, ctypes.c_void_p(d.data_ptr()), nat.F32, e.n, 1))
+            else:
+                e.set_field("T_air", t0, index=0)
+            e.run(1, frames=np.zeros(1, dtype=np.int32))
+            short = e.nan_safe_launches()
+            e.run(24)
+            e.sync()
+            long_ = e.nan_safe_launches()
+            out = e.get_outputs()
+            elev = e.get_field("elev", dtype=np.float32)
+            elev[3] = np.nan
+            if device:
+                d2 = torch.as_tensor(elev, device="cuda:0")
+                torch.cuda.synchronize()
+                e._chk(e.lib.tfg_set_field(e.h, nat.FIELD["elev"], 0, ctypes.c_void_p(d2.data_ptr()), nat.F32, e.n, 1))
+            else:
+                e.set_field("elev", elev)
+            e.run(24)
+            e.sync()
+            runs.append((short, long_, e.nan_safe_launches(), out, e.get_outputs()))
+        finally:
+            e.close()
+    (ha, hb, hc, ho1, ho2), (da, db, dc, do1, do2) = runs
+    assert (ha, hb, hc) == (0, 0, 1)  # host sets are checked at once: clean, clean, then the NaN raster
+    assert (da, db, dc) == (1, 1, 2)  # device sets: the short launch NaN-safe, the long one checked clean
+    np.testing.assert_array_equal(ho1, do1)
+    np.testing.assert_array_equal(ho2, do2)

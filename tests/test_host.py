@@ -241,7 +241,9 @@ def test_bmi_surface_without_gpu():
 
 def test_bmi_grid_topology_of_the_raster():
     """The uniform raster's coordinates and quad topology (additive BMI 2.0
-    methods the reference leaves unimplemented)."""
+    methods the reference leaves unimplemented).  Row 0 is the northern edge,
+    as the engine's halos have it (halo_north pairs with row 0): y falls with
+    the row index, and faces run counter-clockwise in (x, y)."""
     from types import SimpleNamespace
 
     from topoflow_glacier import BmiTopoflowGlacier
@@ -252,7 +254,8 @@ def test_bmi_grid_topology_of_the_raster():
     ny, nx = 3, 4
     assert m.get_grid_node_count(0) == 12 and m.get_grid_size(0) == 12
     np.testing.assert_array_equal(m.get_grid_x(0, np.zeros(nx)), [0, 500, 1000, 1500])
-    np.testing.assert_array_equal(m.get_grid_y(0, np.zeros(ny)), [0, 500, 1000])
+    np.testing.assert_array_equal(m.get_grid_y(0, np.zeros(ny)), [1000, 500, 0])  # row 0 = north
+    np.testing.assert_array_equal(m.get_grid_origin(0, np.zeros(2)), [0, 0])  # the south-west node
     with pytest.raises(NotImplementedError):
         m.get_grid_z(0, np.zeros(1))
     ne, nf = m.get_grid_edge_count(0), m.get_grid_face_count(0)
@@ -264,9 +267,10 @@ def test_bmi_grid_topology_of_the_raster():
     fn = m.get_grid_face_nodes(0, np.zeros(4 * nf, np.int64)).reshape(nf, 4)
     fe = m.get_grid_face_edges(0, np.zeros(4 * nf, np.int64)).reshape(nf, 4)
     assert np.all(m.get_grid_nodes_per_face(0, np.zeros(nf, np.int64)) == 4)
-    x, y = fn % nx, fn // nx
+    x, y = fn % nx, (ny - 1) - fn // nx  # node (row, col) -> (x, y) index with y up: row 0 on top
     area2 = (x * np.roll(y, -1, axis=1) - np.roll(x, -1, axis=1) * y).sum(axis=1)
-    assert np.all(area2 == 2)  # unit squares, counter-clockwise
+    assert np.all(area2 == 2)  # unit squares, counter-clockwise in (x, y)
+    assert np.all(y[:, 0] == y.min(axis=1)) and np.all(x[:, 0] == x.min(axis=1))  # from the lower-left node
     for k in range(4):  # edge k of a face joins its nodes k and k + 1
         a, b = fn[:, k], fn[:, (k + 1) % 4]
         assert all(sorted(en[e]) == sorted((i, j)) for e, i, j in zip(fe[:, k], a, b))

@@ -72,6 +72,30 @@ def test_sharded_oracle_gloo_world2(tmp_path):
         np.testing.assert_array_equal(stitched, ref[k][-1])
 
 
+def test_config5_catchment_diagnostics_gloo_world2(tmp_path):
+    """BASELINE config 5's per-catchment mass balance in its sharded form:
+    bench.py's 43-catchment block raster over a row-blocked grid, dt = 0.25 h;
+    each rank's [44][6] per-catchment integrals (oracle, binned) combined by
+    allreduce_diagnostics over gloo equal the whole grid's."""
+    import bench
+    from tests.harness import catchment_diag, synthetic_inputs
+
+    ny, nx, steps = 16, 32, 24
+    ranks = _torchrun("catch", tmp_path, ny=ny, nx=nx, steps=steps)
+    _, m = oracle_synthetic(11, ny, nx, steps, 24, cfg_over={"dt": 0.25})
+    syn, _ = synthetic_inputs(11, ny, nx, 24)
+    cid = bench.catchment_blocks(0, ny, ny, nx, 43)
+    whole = catchment_diag(syn, m, cid, steps, 24, 44, {"dt": 0.25})
+    assert set(np.unique(cid)) == set(range(43))  # every catchment id occurs in the grid
+    np.testing.assert_array_equal(np.concatenate([r["cid"] for r in ranks]), cid)
+    for r in ranks:
+        assert r["reduced"].shape == (44, 6)
+        np.testing.assert_array_equal(r["reduced"], ranks[0]["reduced"])
+        assert _rel(r["reduced"][:, :5], whole[:, :5]) <= 1e-13
+        np.testing.assert_array_equal(r["reduced"][:, 5], whole[:, 5])
+    assert np.all(whole[:43, 0] > 0) and np.all(whole[43] == 0)
+
+
 @pytest.mark.gpu
 def test_sharded_engine_gloo_world2(tmp_path):
     ny, nx, steps = 64, 96, 48
@@ -102,6 +126,11 @@ def test_rccl_paths_world1(tmp_path):
     z = dict(np.load(tmp_path / "rank0.npz"))
     assert str(z["backend"]) == "nccl"
     np.testing.assert_array_equal(z["diag_out"], z["diag_in"])
+    # 43 catchments (+1 spare row) of a config-5 shard through the RCCL all-reduce
+    assert z["catch_diag_in"].shape == (44, 6)
+    np.testing.assert_array_equal(z["catch_diag_out"], z["catch_diag_in"])
+    present = z["catch_diag_in"][:43, 0] > 0  # the shard's rows hold some of the 43 block catchments
+    assert present.sum() >= 4 and np.all(z["catch_diag_in"][43] == 0)
     if "p2p_refused" in z:
         print("self point-to-point refused:", z["p2p_refused"])
     else:

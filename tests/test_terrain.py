@@ -34,6 +34,25 @@ def test_terrain_oracle_conventions():
     assert np.array_equal(top[0], full[0][10:25]) and np.array_equal(top[1], full[1][10:25])
 
 
+def test_bmi_y_axis_matches_the_terrain_row_order():
+    """The BMI grid coordinates and the engine's stencil agree on north: a DEM
+    that rises with the BMI y coordinate (get_grid_y) rises to the north in
+    the terrain restatement, whose row 0 is the northern edge (halo_north pairs
+    with it), so its downslope aspect points south (-pi/2)."""
+    from types import SimpleNamespace
+
+    from topoflow_glacier import BmiTopoflowGlacier
+
+    m = BmiTopoflowGlacier()
+    m.ny, m.nx, m.n_cells = 6, 7, 42
+    m.cfg = SimpleNamespace(da=0.0009, dx=30.0, dy=30.0)
+    y = m.get_grid_y(0, np.zeros(6))
+    dem = np.repeat((0.1 * y)[:, None], 7, axis=1)  # 0.1 m per metre northward
+    s, a = terrain_oracle(dem, 30.0, 30.0)
+    I = (slice(1, -1), slice(1, -1))
+    assert np.allclose(s[I], 0.1) and np.allclose(a[I], -np.pi / 2)
+
+
 def test_halo_exchange_gloo_world2(tmp_path):
     ny, nx = 9, 16
     ranks = _torchrun("halo", tmp_path, ny=ny, nx=nx, steps=1)

@@ -589,7 +589,8 @@ struct tfg_handle {
   void* forc = nullptr;
   void* stat = nullptr;
   void* lwsw = nullptr;          // [2][n_pad] R, not read by the physics
-  float* geo = nullptr;          // fast engine: [5][n_pad] f32 + [2][n_pad] f64 solar geometry; exact: [6][n_pad] f64 CellStatic
+  float* geo = nullptr;          // fast engine: [5][n_pad] f32 + [2][n_pad] f64 solar geometry; exact: [kStaticPlanes][n_pad] f64 CellStatic
+                                 // (elev, cos_leq, sin_leq, dlon, tan_eq, cos_dlon, sin_dlon)
   bool geo_dirty = true;
   int32_t* catch_id = nullptr;
   double* st = nullptr;
@@ -742,6 +743,13 @@ template <class T>
 uint8_t host_finite(const T* p, int64_t n) {
   bool bad = false;
   for (int64_t i = 0; i < n; ++i) bad |= !std::isfinite(p[i]);
+  return bad ? kDirty : kOk;
+}
+// fp64 host values the fp32 engine will hold: finite after the conversion (a
+// finite double beyond FLT_MAX becomes inf in the frame)
+uint8_t host_finite_as_f32(const double* p, int64_t n) {
+  bool bad = false;
+  for (int64_t i = 0; i < n; ++i) bad |= !std::isfinite((float)p[i]);
   return bad ? kDirty : kOk;
 }
 
@@ -1212,7 +1220,9 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     if (int rc = ensure_qc(h)) return rc;
     if (int rc = upload(h, h->qc, h->engine, src, src_dtype, n, src_on_device)) return rc;
     h->qc_on = true;
-    if (track) return check_finite(h, h->qc, h->engine, n, &h->qc_state);
+    // device sources stay stream-ordered: their status is checked lazily before a launch (choose_form)
+    if (track && src_on_device) h->qc_state = kUnknown;
+    else if (track) return check_finite(h, h->qc, h->engine, n, &h->qc_state);
     return TFG_OK;
   }
   if (field == TFG_ST_WINDOW) {
@@ -1224,7 +1234,9 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
                        h->dp.qscale);
     HIPCHK(h, hipGetLastError());
     h->tot_dirty = true;
-    if (track) {  // a NaN slot makes the window dirty; a finite one leaves the state's status as it was
+    if (track && src_on_device) {
+      h->state_state = kUnknown;  // checked lazily (choose_form -> check_state reads the rebuilt totals)
+    } else if (track) {  // a NaN slot makes the window dirty; a finite one leaves the state's status as it was
       uint8_t st = kOk;
       if (int rc = check_finite(h, h->wtmp, TFG_F64, n, &st)) return rc;
       if (st != kOk) h->state_state = kDirty;
@@ -1246,7 +1258,9 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
     double* sd = h->st + (field == TFG_OUT_H_SNOW ? S_HSNOW : S_HICE) * h->n_pad;
     int rc = upload(h, sd, TFG_F64, src, src_dtype, n, src_on_device);
     if (rc) return rc;
-    if (track) {
+    if (track && src_on_device) {
+      h->state_state = kUnknown;
+    } else if (track) {
       uint8_t st = kOk;
       if (int rc2 = check_finite(h, sd, TFG_F64, n, &st)) return rc2;
       if (st != kOk) h->state_state = kDirty;
@@ -1255,14 +1269,25 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
   }
   int rc = upload(h, dst, fdt, src, src_dtype, n, src_on_device);
   if (rc) return rc;
+  // Finite-data status of what was written (tfg_handle::plane_state).  A host
+  // source is checked now (its upload is synchronous anyway); a device source
+  // keeps the set stream-ordered and non-blocking: its plane is marked
+  // unknown and checked lazily before a launch long enough to pay for it
+  // (choose_form), or the launch runs the NaN-safe form.
+  const bool state_field = field == TFG_OUT_H_SWE || field == TFG_OUT_H_IWE || field == TFG_ST_ECCS ||
+                           field == TFG_ST_ECCI || field == TFG_ST_ALBEDO || field == TFG_ST_NDAYS;
   if (track && is_frame_field(field)) {
     const int plane = field == TFG_IN_P ? F_P : field == TFG_IN_T_AIR ? F_T : field == TFG_IN_HUM_SP ? F_Q
                     : field == TFG_IN_P_AIR ? F_PA : F_UZ;
-    if (int rc2 = check_finite(h, dst, fdt, n, &h->plane_state[(size_t)index * kNumForc + plane])) return rc2;
+    uint8_t* ps = &h->plane_state[(size_t)index * kNumForc + plane];
+    if (src_on_device) *ps = kUnknown;
+    else if (int rc2 = check_finite(h, dst, fdt, n, ps)) return rc2;
   } else if (track && field == TFG_ST_ELEV) {
-    if (int rc2 = check_finite(h, dst, fdt, n, &h->elev_state)) return rc2;
-  } else if (track && (field == TFG_OUT_H_SWE || field == TFG_OUT_H_IWE || field == TFG_ST_ECCS || field == TFG_ST_ECCI ||
-                       field == TFG_ST_ALBEDO || field == TFG_ST_NDAYS)) {
+    if (src_on_device) h->elev_state = kUnknown;
+    else if (int rc2 = check_finite(h, dst, fdt, n, &h->elev_state)) return rc2;
+  } else if (track && state_field && src_on_device) {
+    h->state_state = kUnknown;
+  } else if (track && state_field) {
     uint8_t st = kOk;
     if (int rc2 = check_finite(h, dst, fdt, n, &st)) return rc2;
     if (st != kOk) h->state_state = kDirty;
@@ -1443,6 +1468,8 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
   }
   if (h->qc_on && h->qc_state == kUnknown && check)
     if (int rc = check_finite(h, h->qc, h->engine, h->n, &h->qc_state)) return rc;
+  if (h->elev_state == kUnknown && check)  // a device-sourced elevation raster (tfg_set_field)
+    if (int rc = check_finite(h, h->stat, h->engine, h->n, &h->elev_state)) return rc;
   *ns = h->force_ns ||
         !(inputs_ok && h->state_state == kOk && h->elev_state == kOk && (!h->qc_on || h->qc_state == kOk));
   return TFG_OK;
@@ -1645,7 +1672,7 @@ int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int
     for (int f = 0; f < 5; ++f) {
       uint8_t st = kUnknown;
       if (!src_on_device)
-        st = src_dtype == TFG_F64 ? host_finite(static_cast<const double*>(src) + (size_t)f * n, n)
+        st = src_dtype == TFG_F64 ? host_finite_as_f32(static_cast<const double*>(src) + (size_t)f * n, n)
                                   : host_finite(static_cast<const float*>(src) + (size_t)f * n, n);
       h->plane_state[(size_t)frame * kNumForc + map[f]] = st;
     }

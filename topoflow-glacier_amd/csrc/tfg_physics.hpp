@@ -837,6 +837,18 @@ __device__ __forceinline__ double add_rounded(double h, double a, double b) {
   return h + a * b;
 }
 
+// Cold content a snowfall brings (:1507-1537): rho_s Cp_s (P_snow dt ws)
+// (T0 - T_wb), with Stull's wet-bulb temperature of RH as a fraction (the
+// reference's quirk), fp32: melt_core's increment, for the diagnostic build
+// (melt_core keeps its own copy of the expression, which compiles to the
+// instruction sequence the PMC profiles were measured on).
+__device__ __forceinline__ float snowfall_cold(const DevParams& p, float P_snow, float rh, float T_air) {
+  const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
+                     fast_atanf(rh - 1.676331f) +
+                     (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
+  return p.f_c_eccs * P_snow * (p.f_T0 - T_wb);
+}
+
 // Per-cell partial sums of the fast variant over one launch's steps (fp32;
 // scaled and added to the fp64 accumulators once per cell, padding excluded).
 struct DiagF {
@@ -886,6 +898,7 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P
   const double SM = ts * (1.0 / 3600.0);
   h_swe = dmax<NS>(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
   // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
+  // (snowfall_cold spells out the same increment for the diagnostic build)
   double Eccs = Eccs0;
   if (P_snow > 0.0f) {
     const float rh = RH;
@@ -1093,6 +1106,15 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
 #if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
   const float dbg[13] = {(float)Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
   o.RH = dbg[TFG_DEBUG_TERM];
+#endif
+#if defined(TFG_DEBUG_TERMS)  // diagnostic builds only (tests/diagnostics/term_attribution.py): the
+                              // step's energy terms replace the six outputs; the state evolves as usual
+  o.h_snow = Qn_SW;
+  o.SM = Qn_LW;
+  o.h_ice = Qh;
+  o.IM = Qe;
+  o.M_total = P_snow > 0.0f ? snowfall_cold(p, P_snow, RH, T_air) : 0.0f;
+  o.RH = (float)Q_sum;
 #endif
 }
 

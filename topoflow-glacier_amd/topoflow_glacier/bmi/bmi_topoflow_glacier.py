@@ -609,14 +609,19 @@ class BmiTopoflowGlacier(BmiBase):
     # Node coordinates and quad topology of the uniform raster (BMI 2.0), for
     # callers that walk every grid the same way.  The reference leaves these
     # unimplemented (bmi_base.py); they are additive.  Nodes are numbered row
-    # by row (index = row * nx + col, the layout of every value array); edges
-    # are the nx - 1 x-edges of each row, then the nx y-edges of each row pair;
-    # faces are the cells between four nodes, counter-clockwise from the
-    # lower-left node, with edges in the same order.
+    # by row (index = row * nx + col, the layout of every value array), and
+    # row 0 is the NORTHERN edge, as in the engine: tfg_terrain_from_dem and
+    # the conduction and ice-flow halos pair halo_north with row 0.  So y
+    # decreases with the row index: row k sits at y = (ny - 1 - k) * dy above
+    # the origin (get_grid_origin), the lower-left (south-west) node.  Edges
+    # are the nx - 1 x-edges of each row, then the nx y-edges of each row
+    # pair; faces are the cells between four nodes, counter-clockwise in
+    # (x, y) from the lower-left node, with edges in the same order.
     def _axis(self, k: int) -> np.ndarray:
         sp = self.get_grid_spacing(0, np.empty(2))
         n = (self.ny, self.nx)[k]
-        return np.arange(n, dtype=np.float64) * sp[k]
+        a = np.arange(n, dtype=np.float64) * sp[k]
+        return a[::-1].copy() if k == 0 else a
 
     def get_grid_x(self, grid: int, x):
         x[:] = self._axis(1)
@@ -648,7 +653,8 @@ class BmiTopoflowGlacier(BmiBase):
 
     def get_grid_face_nodes(self, grid: int, face_nodes):
         node = np.arange(self.ny * self.nx).reshape(self.ny, self.nx)
-        f = np.stack([node[:-1, :-1], node[:-1, 1:], node[1:, 1:], node[1:, :-1]], axis=-1)
+        # lower-left (row k + 1), lower-right, upper-right (row k), upper-left
+        f = np.stack([node[1:, :-1], node[1:, 1:], node[:-1, 1:], node[:-1, :-1]], axis=-1)
         face_nodes[:] = f.ravel()
         return face_nodes
 
@@ -657,7 +663,8 @@ class BmiTopoflowGlacier(BmiBase):
         n_ex = ny * (nx - 1)
         ex = np.arange(n_ex).reshape(ny, nx - 1)
         ey = n_ex + np.arange((ny - 1) * nx).reshape(ny - 1, nx)
-        f = np.stack([ex[:-1, :], ey[:, 1:], ex[1:, :], ey[:, :-1]], axis=-1)
+        # bottom (row k + 1), right, top (row k), left: edge j joins face nodes j and j + 1
+        f = np.stack([ex[1:, :], ey[:, 1:], ex[:-1, :], ey[:, :-1]], axis=-1)
         face_edges[:] = f.ravel()
         return face_edges
 

@@ -172,9 +172,25 @@ class GlacierEngine:
             self.set_field("window", z["window"][j], index=j)
         self.step_index = int(z["step_index"])
 
-    def set_inputs(self, values: np.ndarray, index: int = 0) -> None:
+    def set_inputs(self, values, index: int = 0) -> None:
         """The five physics inputs of one frame in one call: values [5][n] in
-        BMI order P_air, Hum_sp, P, T_air, uz (tfg_set_inputs)."""
+        BMI order P_air, Hum_sp, P, T_air, uz (tfg_set_inputs): a host array,
+        or a contiguous float32 / float64 torch CUDA tensor, which the engine
+        reads on its own stream (ordered after torch's current stream when the
+        two differ; the caller keeps the tensor alive until the step has run
+        or the engine is synced)."""
+        if getattr(values, "is_cuda", False):
+            import torch
+
+            if tuple(values.shape) != (5, self.n) or not values.is_contiguous():
+                raise ValueError(f"inputs must be a contiguous [5][{self.n}] tensor")
+            code = {torch.float32: nat.F32, torch.float64: nat.F64}[values.dtype]
+            own = getattr(self, "_stream_ptr", None)
+            same = own is not None and own == torch.cuda.current_stream(values.device).cuda_stream
+            if not same:
+                torch.cuda.current_stream(values.device).synchronize()
+            self._chk(self.lib.tfg_set_inputs(self.h, int(index), ctypes.c_void_p(values.data_ptr()), code, self.n, 1))
+            return
         a = np.ascontiguousarray(values, dtype=np.float64)
         if a.shape != (5, self.n):
             raise ValueError(f"inputs must be [5][{self.n}]")
