@@ -83,7 +83,7 @@ MIN_LAUNCHES = 6
 # Why 6: the first launch after the barrier that opens the timed region runs
 # 0.5-3.6 ms long at every shape and warm-up length (profiles/r3c_slab_skew_study.jsonl,
 # profiles/r3f_slab_depth_study.jsonl); over 6 launches it weighs ~1 % on the
-# 1024 x 8192 slab instead of ~2 % over 3.
+# 1024 x 8192 slab instead of ~2 % over 3 (HISTORY.md section 6).
 # auto launch depth by shard size, as deep as ~210 GB of output slots allow
 # (hist_depth = launch depth): 128 steps above 2^25 cells (the 8192^2 grid: the
 # 128 slots take 206 GB, the whole footprint 266 GB; 96-step launches ran 1.0 %

@@ -211,7 +211,7 @@ def fp64_baseline_flips(c_out: dict, ref: dict, rtol: float = 1e-5) -> int:
 # max(Q_sum dt - Eccs, 0) (:1364-1368): where the step's energy just exceeds the
 # cold content the difference cancels.  Both sides of it carry the error of
 # the fp32 flux terms (a few 1e-7 of their magnitude: hardware exp2/log2/rcp,
-# polynomial atan; mean bias -4e-8): E_in of this step, and
+# polynomial atan; mean bias -4e-8, HISTORY.md section 3): E_in of this step, and
 # Eccs, which integrates E_in over the steps before.  Such a mismatch is
 # explained when SM and M_total (:1441) differ by no more than 1e-6 of the
 # energy moved so far, sum over steps <= k of |Qn_SW| + |Qn_LW| + |Qh| + |Qe|,

@@ -30,7 +30,7 @@ SRC = ROOT / "tests" / "native" / "fastmath_host.cpp"
 HEADER = ROOT / "topoflow-glacier_amd" / "csrc" / "tfg_fastmath.hpp"
 EXP, EXP_LIBM, LOG, LOG_LIBM, DIV_61121, DIV_3600, EXP_SGPR = 3, 4, 5, 6, 7, 8, 9
 
-# the bounds DESIGN.md section 5 states (ulps of numpy's result)
+# the bounds HISTORY.md section 5 states (ulps of numpy's result)
 EXP_ULPS = 1.0
 LOG_ULPS = 1.0
 

@@ -126,7 +126,7 @@ __device__ __forceinline__ void cond_lds_barrier() { asm volatile("s_waitcnt lgk
 #define TFG_COND_ROWS 64
 #endif
 #ifndef TFG_COND_AHEAD
-#define TFG_COND_AHEAD 2  // rows requested beyond the next one while a row is evaluated (1 or 2; 2: 510 against 514-516 us at 8192^2)
+#define TFG_COND_AHEAD 2  // rows requested beyond the next one while a row is evaluated (1 or 2; 2: 510 against 514-516 us at 8192^2, HISTORY.md section 6)
 #endif
 constexpr int kCondTX = 256, kCondOut = kCondTX - 2, kCondRows = TFG_COND_ROWS;
 

@@ -1019,7 +1019,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // allocations of one 4096^2 shard in one process, 113.8-116.0 with 512 cells
   // (2 KB) of skew; 1024 x 8192: 111.9-114.1 against 113.7-115.2; 8192^2:
   // 116.4-117.4 against 117.2-117.5 (tests/diagnostics/alloc_variance.py,
-  // DESIGN.md section 5).  TFG_PLANE_SKEW=<cells> overrides it (measurement).
+  // HISTORY.md section 5).  TFG_PLANE_SKEW=<cells> overrides it (measurement).
   int64_t skew = h->n_pad >= ((int64_t)1 << 20) ? kPlaneSkew : 0;
   if (const char* e = std::getenv("TFG_PLANE_SKEW")) skew = round_up(std::max<int64_t>(0, atoll(e)), 64);
   h->n_pad += skew;
@@ -1049,7 +1049,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // which hides the latency bubble at the start of every cell; measured
   // +9 % for 128 per CU over 8 (round 1), and with the two-step prefetch
   // +0.6 % for 512 over 128 at 8192^2, +0.6 % on the 4096 x 8192 shard, even
-  // at 4096^2 (where the chunk count caps it at 256 per CU; DESIGN.md
+  // at 4096^2 (where the chunk count caps it at 256 per CU; HISTORY.md
   // section 5).  The per-workgroup diagnostic slab is kept under 256 MiB for
   // large catchment counts: 65536 workgroups at config 5's 43 catchments
   // (135 MB), +1.2 % on its slab against the 16384 a 64 MiB cap gave.

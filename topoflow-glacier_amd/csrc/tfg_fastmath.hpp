@@ -1,5 +1,5 @@
 // tfg_fastmath.hpp -- fp64 exp, log and division by a constant for the fp64
-// ("exact") engine.  The fp64 step is issue-bound (1450
+// ("exact") engine.  The fp64 step is issue-bound (HISTORY.md section 5: 1450
 // VALU instructions per wave and cell-step at ~90 % of the vector pipe before
 // this file); per step it evaluates eight exp, three log and about fifteen
 // divisions by a model constant.

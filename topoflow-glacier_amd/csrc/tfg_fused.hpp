@@ -375,7 +375,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       };
       auto advance = [&](int k, const Frame& f) {
         // SGPR spills 62 -> 56 (fp32) and 170 -> 111 (fp64); same-box A/B:
-        // fp32 -0.6 % and fp64 -3.4 % time per launch.
+        // fp32 -0.6 % and fp64 -3.4 % time per launch (HISTORY.md section 5).
         TFG_STEP_PARAMS(p);
         const tfg_uniforms* up = uni + k;
         const tfg_uniforms u = *up;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       };
       // The fast engine requests two steps ahead (three register sets, loop
       // unrolled by three, 127 VGPRs): +1.2-2.6 % at 1024^2, 2048^2 and 8192^2
-      // in same-box A/Bs against one step ahead.  Step
+      // in same-box A/Bs against one step ahead (HISTORY.md section 5).  Step
       // k + 2's window slot is then read before steps k and k + 1 write theirs,
       // so a fused launch needs ring_len > 2 (launch_steps runs shorter windows
       // one step per launch).  The conduction (QC) and NaN-safe (NS) forms keep

@@ -1,16 +1,19 @@
 """Row-block decomposition of a raster over the GPUs of one node.
 
-The one stencil on the path -- slope/aspect from a DEM (tfg_terrain_from_dem,
-SURVEY.md 8(f) row 4) -- needs the elevation row on each side of a shard: a
-one-row halo exchanged point-to-point between neighbouring ranks
-(:func:`exchange_halo_rows`, RCCL send/recv over xGMI on the GPU path).
-
 Cells are independent in the reference physics (no lateral term: Qc = Qa = 0,
-bmi_topoflow_glacier.py:936-955), so a time step needs no data exchange
-between shards.  The only cross-shard operation is the mass-balance
-diagnostics (vol_P/PR/PS/SM/IM sums and the P_max max, :558-624,
-:1482-1494), combined on demand with one all-reduce over
+bmi_topoflow_glacier.py:936-955), so a time step of the energy balance needs
+no data exchange between shards.  Its only cross-shard operation is the
+mass-balance diagnostics (vol_P/PR/PS/SM/IM sums and the P_max max,
+:558-624, :1482-1494), combined on demand with one all-reduce over
 ``torch.distributed`` (RCCL over xGMI on MI355X; gloo in CPU tests).
+
+Three optional stencils (none in the reference
+physics) need the rows on each side of a shard, swapped point-to-point
+between neighbouring ranks by :func:`exchange_halo_rows` (RCCL send/recv
+over xGMI on the GPU path): slope/aspect from a DEM (once,
+:func:`terrain_from_dem_sharded`), lateral heat conduction (once per
+conduction interval, :func:`lateral_conduction`) and ice flow (before every
+sub-step, overlapped with the interior strips, :func:`ice_flow`).
 """
 
 from __future__ import annotations
