@@ -1,0 +1,351 @@
+"""A numpy float32 emulation of the fp32 engine's step (csrc/tfg_physics.hpp
+cell_step_fast + melt_core), for CPU experiments on its accuracy.
+Diagnostic only: no test relies on it, and it is not the engine.
+
+It follows the kernel's operation order with numpy float32 arithmetic; the
+hardware v_exp_f32 / v_log_f32 / v_rcp_f32 are stood in for by correctly
+rounded float32 exp2 / log2 / division, and fmaf by a float64 product-sum
+rounded once.  So it carries the fp32 engine's rounding structure, but not
+the approximation error of the gfx950 transcendental instructions (~1 ulp,
+log biased by -0.44 ulp), and its miss rates are a lower bound of the GPU's.
+
+`promote` switches term groups to fp64, as a kernel variant would:
+  "lw"    T_K, T_surf_K and the long-wave balance in fp64 (em_air stays fp32)
+  "em"    em_air's power (e/T)^(1/7) in fp64
+  "dew"   e_air, the dew point and T_air - T_surf in fp64
+  "sum"   the flux sum and E_in in fp64
+  "sw"    albedo and Qn_SW in fp64
+  "turb"  Dn, Dh, Ri and the turbulent fluxes in fp64
+  "de"    the vapour-pressure difference (e_air - e_surf) in fp64
+  "wb"    the snowfall cold content in fp64
+  "all"   every flux in fp64
+
+  python tests/diagnostics/fp32_emulation.py [cells] [steps] [variant,variant,...]
+prints, per variant, the fraction of cell-steps beyond pure-relative 1e-5 of
+the numpy oracle (cells with a melt-out flip compared up to the flip, as
+bench.py's parity check does).
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(ROOT / "topoflow-glacier_amd"), str(ROOT / "oracle"), str(ROOT)]
+
+f32, f64 = np.float32, np.float64
+LOG2E, LN2 = f32(1.4426950408889634), f32(0.6931471805599453)
+HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
+
+
+def fma32(a, b, c):
+    return (np.asarray(a, f64) * np.asarray(b, f64) + np.asarray(c, f64)).astype(f32)
+
+
+def exp2_32(x):
+    return np.exp2(np.asarray(x, f64)).astype(f32)
+
+
+def log2_32(x):
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.log2(np.asarray(x, f64)).astype(f32)
+
+
+def rcp32(x):
+    return (f32(1.0) / np.asarray(x, f32)).astype(f32)
+
+
+def log2_nr(x):
+    y = log2_32(x)
+    return fma32(fma32(x, exp2_32(-y), f32(-1.0)), LOG2E, y)
+
+
+def ln_c(x64):
+    """ln(x) as a kernel could afford it: the fp32 log2 (Newton-refined) of
+    x rounded to fp32, plus the fp64 first-order correction for that rounding."""
+    x64 = np.asarray(x64, f64)
+    xf = x64.astype(f32)
+    return f64(log2_nr(xf)) * np.log(2.0) + (x64 - f64(xf)) / f64(xf)
+
+
+def atan32(x):
+    return np.arctan(np.asarray(x, f64)).astype(f32)
+
+
+class Fp32Engine:
+    """The fp32 engine's per-cell state and step, vectorised over cells."""
+
+    def __init__(self, cfg, static, promote=()):
+        import tfg_oracle as O
+
+        c = dict(O.CFG_DEFAULTS)
+        c.update(cfg)
+        self.c, self.promote = c, set(promote)
+        if "all" in self.promote:
+            self.promote |= {"lw", "em", "dew", "sum", "sw", "turb", "de", "wb"}
+        dt = f64(c["dt"])
+        self.dt = dt
+        self.ws = f64(c["rho_H2O"]) / f64(c["rho_snow"])
+        self.wi = f64(c["rho_H2O"]) / f64(c["rho_ice"])
+        self.rho_Lf = f64(c["rho_H2O"]) * f64(c["Lf"])
+        self.inv_dt_rhoLf = 1.0 / (dt * self.rho_Lf)
+        self.c_sm3600 = 3600.0 / (dt * self.rho_Lf)
+        self.dt3600 = dt * 3600.0
+        # host folds (tfg_engine.hip derive_params)
+        self.f_eps100, self.f_ome100 = f32(100 * c["eps"]), f32(100 * (1 - c["eps"]))
+        self.f_gz, self.f_inv_z0 = f32(c["g"] * 10.0), f32(1.0 / c["z0_air"])
+        self.f_k2 = f32((c["kappa"] / np.log(2.0)) ** 2)
+        self.f_rcp = f32(c["rho_air"] * c["Cp_air"])
+        self.f_qe = f32(c["rho_air"] * c["Lv"] * c["latent_heat_constant"] * 100.0 / c["sea_level_p0"])
+        self.f_dust, self.f_1pdust = f32(c["dust_atten"]), f32(1 + c["dust_atten"])
+        F, C = c["canopy_factor"], c["cloud_factor"]
+        self.ccF = (1 - F) * 1.72 * (1.0 + 0.22 * C * C)
+        self.f_ccF, self.f_F = f32(self.ccF), f32(F)
+        self.em_s_sigma = c["em_surf"] * c["sigma"]
+        self.f_em_s_sigma = f32(self.em_s_sigma)
+        self.f_qfac = f32(dt * self.ws * 2.0 ** 36)
+        self.f_dt, self.f_T0 = f32(dt), f32(c["T0"])
+        self.f_c_eccs = f32(c["rho_snow"] * c["Cp_snow"] * dt * self.ws)
+        self.thr_q = int(np.ceil(0.03 * 2.0 ** 36))
+        self.dpd = dt / 86400.0
+        # per-cell geometry (derive_geo), fp64 then fp32 planes
+        lat = f64(c["lat"]) * (np.pi / 180.0)
+        sin_lat, cos_lat = np.sin(lat), np.cos(lat)
+        elev, slope, aspect = (np.asarray(static[k], f64) for k in ("elev", "slope", "aspect"))
+        ca, sa = np.sin(aspect), np.cos(aspect)  # sincos(aspect, &ca, &sa): alpha = pi/2 - aspect
+        r = 1.0 / np.sqrt(1.0 + slope * slope)
+        sb, cb = slope * r, r
+        sl = sb * ca * cos_lat + cb * sin_lat
+        cl = np.sqrt(np.maximum(1.0 - sl * sl, 0.0))
+        t = (sb * sa) / (cb * cos_lat - sb * sin_lat * ca)
+        rt = 1.0 / np.sqrt(1.0 + t * t)
+        self.ek = (-(-c["M_mass_air"] * c["g"]) / c["uni_gas_const"] * elev * 1.4426950408889634).astype(f32)
+        self.ek64 = -(-c["M_mass_air"] * c["g"]) / c["uni_gas_const"] * elev
+        self.sl, self.cc, self.cs = sl.astype(f32), (cl * rt).astype(f32), (cl * t * rt).astype(f32)
+        self.dlon = np.arctan(t)
+        self.tan_eq = sl / cl
+        self.t_noon = -1.0 * self.dlon / (np.pi / 12)
+        # state (initialize :344-395)
+        n = elev.size
+        self.h_snow, self.h_ice = np.asarray(static["h0_snow"], f64).copy(), np.asarray(static["h0_ice"], f64).copy()
+        self.h_swe, self.h_iwe = np.asarray(static["h0_swe"], f64).copy(), np.asarray(static["h0_iwe"], f64).copy()
+        self.Eccs = np.maximum(f64(c["rho_snow"]) * f64(c["Cp_snow"]) * self.h_snow * (f64(c["T0"]) - 0.0), 0.0)
+        self.Ecci = np.full(n, max((f64(c["rho_ice"]) * f64(c["Cp_ice"])) * f64(c["h_active_layer"]) * f64(c["T0"]), 0.0))
+        self.albedo = np.full(n, 0.3)
+        self.n = np.zeros(n)
+        self.ring = np.zeros((int(3 * 24 / dt), n), np.int32)
+        self.slot = 0
+        self.tot = np.zeros(n, np.int64)
+
+    def step(self, u, P, T_air, Hum_sp, P_air, uz):
+        c, pr = self.c, self.promote
+        P, T_air, Hum_sp, P_air, uz = (np.asarray(x, f32) for x in (P, T_air, Hum_sp, P_air, uz))
+        snow_pos, ice_pos = self.h_snow > 0, self.h_ice > 0
+        T_K = T_air + f32(273.15)
+        rT = rcp32(T_K)
+        is_rain = T_air > f32(c["T_rain_snow"])
+        P_rain = np.where(is_rain, P, f32(0))
+        P_snow = np.where(is_rain, f32(0), P)
+        rA = rcp32(T_air + f32(237.3))
+        inv_esat = f32(1.0 / 6.11) * exp2_32((f32(-17.3) * LOG2E) * T_air * rA)
+        e_air = Hum_sp * P_air * rcp32(self.f_eps100 + self.f_ome100 * Hum_sp)
+        RH = e_air * inv_esat
+        if "dew" in pr or "dewc" in pr:
+            e64 = f64(Hum_sp) * f64(P_air) / (100 * c["eps"] + 100 * (1 - c["eps"]) * f64(Hum_sp))
+            L = np.log(e64 / 6.1121) if "dew" in pr else ln_c(e64 * (1 / 6.1121))
+            T_dew64 = 257.14 * L / (18.678 - L)
+            T_surf64 = np.where(snow_pos | ice_pos, np.minimum(T_dew64, 0.0), T_dew64)
+            dTs64 = f64(T_air) - T_surf64
+            T_dew, T_surf, dTs = T_dew64.astype(f32), T_surf64.astype(f32), dTs64.astype(f32)
+            self.e64 = e64
+            if "r" in pr:  # the kernel keeps only the fp32-rounded results (register pressure)
+                T_surf64, dTs64 = f64(T_surf), f64(dTs)
+        else:
+            log_term = log2_nr(e_air * f32(1 / 6.1121)) * LN2
+            T_dew = f32(257.14) * log_term * rcp32(f32(18.678) - log_term)
+            T_surf = np.where(snow_pos | ice_pos, np.minimum(T_dew, f32(0)), T_dew)
+            dTs = T_air - T_surf
+            T_surf64, dTs64 = f64(T_surf), f64(dTs)
+        if "turb" in pr or "turbc" in pr:
+            bot = f64(uz) ** 2 * (f64(T_air) + 273.15)
+            bot = np.where(bot == 0, 0.01, bot)
+            Ri = c["g"] * 10.0 * dTs64 / bot
+            ln = np.log if "turb" in pr else ln_c
+            arg = c["kappa"] / ln(np.maximum((10.0 - self.h_snow) / c["z0_air"], 0.01))
+            Dn = f64(uz) * arg * arg
+            Dh64 = np.where(Ri > 0, Dn / (1 + 10 * Ri), Dn * (1 - 10 * Ri))
+            Dh = Dh64.astype(f32)
+            Qh64 = c["rho_air"] * c["Cp_air"] * Dh64 * dTs64
+        else:
+            bot = (uz * uz) * T_K
+            bot = np.where(bot == 0, f32(0.01), bot)
+            Ri = self.f_gz * dTs * rcp32(bot)
+            L2 = log2_32(np.maximum((f32(10) - self.h_snow.astype(f32)) * self.f_inv_z0, f32(0.01)))
+            Dn = uz * self.f_k2 * rcp32(L2 * L2)
+            Dh = np.where(Ri > 0, Dn * rcp32(fma32(f32(10), Ri, f32(1))), Dn * fma32(f32(-10), Ri, f32(1)))
+            Dh64 = f64(Dh)
+            Qh64 = f64(self.f_rcp * Dh * dTs)
+        if "de" in pr:
+            esat = lambda T: 6.11 * np.exp(17.3 * T / (T + 237.3))  # noqa: E731
+            de64 = f64(e_air) * (1.0 - esat(T_surf64) / esat(f64(T_air)))
+            p0f = np.exp(self.ek64 / (f64(T_air) + 273.15))
+            Qe64 = f64(self.f_qe) * Dh64 * de64 * p0f
+        else:
+            rS = rcp32(T_surf + f32(237.3))
+            xs2 = f32(-5922.6815) * dTs * rS * rA
+            de = fma32(-e_air, exp2_32(xs2), e_air)
+            Qe64 = f64(self.f_qe * Dh * de * exp2_32(self.ek * rT))
+        # window + albedo
+        sq = P_snow * self.f_qfac
+        q = np.rint(np.clip(sq, -2147483520.0, 2147483520.0)).astype(np.int64)
+        self.tot += q - self.ring[self.slot]
+        self.ring[self.slot] = q
+        self.slot = (self.slot + 1) % self.ring.shape[0]
+        self.n = np.where(self.tot >= self.thr_q, 0.0, self.n + self.dpd)
+        if "sw" in pr:
+            r64 = np.where(T_air > 0, 0.12, 0.05)
+            snow_alb = 0.4 + 0.44 * np.exp(-self.n * r64)
+            a = np.where(snow_pos, snow_alb, self.albedo)
+        else:
+            r = np.where(T_air > 0, f32(0.12) * LOG2E, f32(0.05) * LOG2E)
+            snow_alb = f32(0.4) + f32(0.44) * exp2_32(-self.n.astype(f32) * r)
+            a = np.where(snow_pos, snow_alb, self.albedo.astype(f32)).astype(f64)
+        a = np.where((self.h_snow == 0) & ice_pos, 0.3, a)
+        a = np.where((self.h_snow == 0) & (self.h_ice == 0), 0.15, a)
+        self.albedo = a
+        # shortwave
+        w = exp2_32((f32(0.0614) * LOG2E) * T_dew)
+        tau = np.minimum(np.maximum(exp2_32(fma32(u["tau_c1"], w, u["tau_c0"])) - self.f_dust, f32(0)), f32(1))
+        gam = self.f_1pdust - exp2_32(fma32(u["gam_c1"], w, u["gam_c0"]))
+        cwl = u["cos_wth_f"] * self.cc - u["sin_wth_f"] * self.cs
+        K_ET = np.maximum(fma32(u["kc_f"], cwl, u["ks_f"] * self.sl), f32(0))
+        kf = f32(u["k_et_flat_f"])
+        K_dif = f32(0.5) * gam * kf
+        albf = a.astype(f32)
+        K_bs = f32(0.5) * gam * albf * fma32(tau, kf, K_dif)
+        K_cs = tau * K_ET + K_dif + K_bs
+        arg = np.clip(-1.0 * self.tan_eq * u["tan_d"], -1.0, 1.0)
+        ac = np.arccos(arg)
+        T_sr = np.maximum(-1.0 * ac / (np.pi / 12) + self.t_noon, u["flat_sr"])
+        T_ss = np.minimum(ac / (np.pi / 12) + self.t_noon, u["flat_ss"])
+        dark = (u["th"] <= T_sr) | (u["th"] >= T_ss)
+        K_cs = np.where(dark, f32(0), K_cs)
+        if "sw" in pr:
+            Qsw64 = f64(K_cs) * (1.0 - a)
+        else:
+            Qsw64 = f64(K_cs * (f32(1) - albf))
+        # longwave
+        if "em" in pr:
+            ex = self.e64 if ("dew" in pr or "dewc" in pr) else f64(e_air)
+            em = self.ccF * ((ex / 10.0) / (f64(T_air) + 273.15)) ** (1 / 7) + f64(self.f_F)
+            if "r" in pr:
+                em = em.astype(f32).astype(f64)
+        else:
+            em = f64(fma32(self.f_ccF, exp2_32(log2_32(e_air * f32(0.1) * rT) * f32(1 / 7)), self.f_F))
+        if "lw" in pr:
+            ta, ts = f64(T_air) + 273.15, T_surf64 + 273.15
+            Qlw64 = self.em_s_sigma * (em * ta ** 4 - ts ** 4)
+        else:
+            TsK = T_surf + f32(273.15)
+            ta2, ts2 = T_K * T_K, TsK * TsK
+            Qlw64 = f64(self.f_em_s_sigma * fma32(em.astype(f32), ta2 * ta2, -(ts2 * ts2)))
+        if "sum" in pr:
+            Q = ((Qsw64 + Qlw64) + Qh64) + Qe64
+            E_in = Q * self.dt
+        else:
+            Q = ((Qsw64.astype(f32) + Qlw64.astype(f32)) + Qh64.astype(f32)) + Qe64.astype(f32)
+            E_in = f64(Q * self.f_dt)
+        self.last = {"Qn_SW": Qsw64, "Qn_LW": Qlw64, "Qh": Qh64, "Qe": Qe64, "Q_sum": f64(Q)}
+        # melt (melt_core)
+        prev_swe = self.h_swe
+        E_rem_s = np.maximum(E_in - self.Eccs, 0.0)
+        h_swe = self.h_swe + f64(P_snow) * self.dt
+        ts_ = np.minimum(E_rem_s * self.c_sm3600, h_swe)
+        SM = ts_ * (1.0 / 3600.0)
+        h_swe = np.maximum(h_swe - SM * self.dt3600, 0.0)
+        Eccs = self.Eccs.copy()
+        sn = P_snow > 0
+        if sn.any():
+            rh = RH
+            if "wb" in pr:
+                R = f64(rh)
+                Ta = f64(T_air)
+                T_wb = (Ta * np.arctan(0.151977 * (R + 8.313659) ** 0.5) + np.arctan(Ta + R) - np.arctan(R - 1.676331)
+                        + (0.00391838 * R ** 1.5) * np.arctan(0.023101 * R) - 4.86035)
+                inc = f64(self.c["rho_snow"]) * f64(self.c["Cp_snow"]) * (f64(P_snow) * self.dt * self.ws) * (
+                    f64(self.c["T0"]) - T_wb)
+            else:
+                T_wb = (T_air * atan32(f32(0.151977) * np.sqrt(rh + f32(8.313659))) + atan32(T_air + rh)
+                        - atan32(rh - f32(1.676331))
+                        + (f32(0.00391838) * (rh * np.sqrt(rh))) * atan32(f32(0.023101) * rh) - f32(4.86035))
+                inc = f64(self.f_c_eccs * P_snow * (self.f_T0 - T_wb))
+            Eccs = np.where(sn, np.maximum(Eccs + inc - E_in, 0.0), Eccs)
+        E_rem_i = np.maximum(E_in - self.Ecci, 0.0)
+        IM = np.where((h_swe == 0) & (prev_swe == 0), E_rem_i * self.inv_dt_rhoLf, 0.0)
+        Ecci = np.maximum(self.Ecci - E_in, 0.0)
+        Ecci = np.where(self.h_ice == 0, 0.0, Ecci)
+        IM = np.minimum(IM, self.h_iwe / self.dt)
+        ti = np.minimum(IM * 3600.0, self.h_iwe)
+        IM = ti * (1.0 / 3600.0)
+        h_iwe = np.maximum(self.h_iwe - IM * self.dt3600, 0.0)
+        Eccs = np.where(~sn, np.maximum(Eccs - E_in, 0.0), Eccs)
+        Eccs = np.where(h_swe * self.ws == 0, 0.0, Eccs)
+        self.h_swe, self.h_iwe, self.Eccs, self.Ecci = h_swe, h_iwe, Eccs, Ecci
+        self.h_snow, self.h_ice = h_swe * self.ws, h_iwe * self.wi
+        SMf, IMf = SM.astype(f32), IM.astype(f32)
+        return {"h_snow": self.h_snow.astype(f32), "SM": SMf, "h_ice": self.h_ice.astype(f32), "IM": IMf,
+                "M_total": IMf + SMf + P_rain * f32(1 / 3600), "RH": RH}
+
+
+def main():
+    import tfg_oracle as O
+
+    from tests.harness import BASE_CFG, melt_out_flips, valid_mask
+    from topoflow_glacier.physics.clock import StepClock
+    from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
+
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 129
+    variants = sys.argv[3].split(",") if len(sys.argv) > 3 else ["", "lw", "em", "dew", "sum", "sw", "turb", "de",
+                                                                  "wb", "all"]
+    syn = synthetic_cells(20251001, np.arange(n), diurnal_table(24))
+    static = {k: np.asarray(syn[s], f64) for k, s in (("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"),
+              ("h0_snow", "h_snow"), ("h0_ice", "h_ice"), ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
+    cfg = dict(BASE_CFG)
+    jd, _, _, tsn = O.oracle_clock(cfg["start_time"], cfg["dt"], steps, cfg["lon"])
+    clk = StepClock(cfg["start_time"], cfg["dt"], cfg["lat"], cfg["lon"], None, ring_len=int(72 / cfg["dt"]))
+    U = clk.uniforms(0, steps)
+    frames = np.arange(steps) % 24
+    m = O.OracleGrid(cfg, **static)
+    ref = {v: np.empty((steps, n)) for v in HIST}
+    for k in range(steps):
+        r = m.step(*(syn[v][frames[k]].astype(f64) for v in ("P", "T_air", "Hum_sp", "P_air", "uz")), jd[k], tsn[k])
+        for v in HIST:
+            ref[v][k] = r[v]
+    out = {}
+    for var in variants:
+        t0 = time.time()
+        e = Fp32Engine(cfg, static, [x for x in var.split("+") if x])
+        g = {v: np.empty((steps, n)) for v in HIST}
+        for k in range(steps):
+            o = e.step(U[k], *(syn[v][frames[k]] for v in ("P", "T_air", "Hum_sp", "P_air", "uz")))
+            for v in HIST:
+                g[v][k] = o[v]
+        flip, genuine = melt_out_flips(g, ref)
+        ok = valid_mask(flip, steps)
+        res = {"flips": int((flip >= 0).sum()), "genuine": len(genuine)}
+        for v in HIST:
+            gv, rv = g[v][ok], ref[v][ok]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
+            res[v] = round(float(np.mean(rel > 1e-5)) * 100, 4)
+        res["s"] = round(time.time() - t0, 1)
+        out[var or "fp32"] = res
+        print(var or "fp32", json.dumps(res), flush=True)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -953,6 +953,62 @@ __device__ __forceinline__ void melt_fast(const DevParams& p, QS Q_sum, float P_
   o.RH = RH;
 }
 
+// fp64 pieces for the fp32 engine's accuracy promotions (TFG_ACC, below).
+// rcp_d: 1/x from v_rcp_f32 and one fp64 Newton step (relative error ~1e-14;
+// x within fp32 range).  ln_d: ln x to ~1e-15 relative for finite x > 0
+// (x = 2^e m, m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh((m-1)/(m+1)) as an odd
+// series to t^11, |t| <= 0.172), the hardware log for 0, inf and NaN (their
+// numpy values: -inf, inf, NaN).  root7_d: x^(1/7) from the fp32 power and one
+// Newton step (relative error ~1e-13).
+__device__ __forceinline__ double rcp_d(double x) {
+  const double r = (double)frcp((float)x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double ln_d(double x) {
+  int e = __builtin_amdgcn_frexp_exp(x);
+  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
+  if (m < 0.70710678118654752) { m = m + m; e -= 1; }
+  const double t = (m - 1.0) * rcp_d(m + 1.0);
+  const double s = t * t;
+  double q = 1.0 / 11.0;
+  q = fma(q, s, 1.0 / 9.0);
+  q = fma(q, s, 1.0 / 7.0);
+  q = fma(q, s, 1.0 / 5.0);
+  q = fma(q, s, 1.0 / 3.0);
+  const double lm = fma(2.0 * t * s, q, 2.0 * t);
+  const double r = fma((double)e, 0.69314718055994531, lm);
+  return (x > 0.0 && x < INFINITY) ? r : (double)(flog2((float)x) * kLn2);
+}
+__device__ __forceinline__ double root7_d(double x) {
+  const double y = (double)fexp2(flog2((float)x) * (1.0f / 7.0f));
+  const double y2 = y * y;
+  const double y6 = y2 * y2 * y2;
+  const double r = fma(x * (1.0 / 7.0), rcp_d(y6), y * (6.0 / 7.0));
+  return (x > 0.0 && x < INFINITY) ? r : y;
+}
+
+// TFG_ACC: a bit mask of fp64 promotions of the fp32 engine's energy terms,
+// ordered by how much of its pure-relative error each removes
+// (tests/diagnostics/fp32_emulation.py, tests/diagnostics/term_attribution.py;
+// DESIGN.md section 3):
+//   1  LW    the long-wave balance (:1231-1248): T + 273.15, the fourth powers
+//            and their difference (LW_in ~ LW_out ~ 300 W m-2 cancel to ~100)
+//   2  DEW   e_air, the dew point, T_surf and T_air - T_surf (:809-911)
+//   4  EM    em_air's (e/T)^(1/7) (:1167)
+//   8  TURB  Ri, Dn, Dh and Qh (:626-745)
+//  16  SUM   the flux sum and E_in (:1259-1319, :1364)
+#ifndef TFG_ACC
+#define TFG_ACC 0
+#endif
+#define TFG_ACC_LW ((TFG_ACC) & 1)
+#define TFG_ACC_DEW ((TFG_ACC) & 2)
+#define TFG_ACC_EM ((TFG_ACC) & 4)
+#define TFG_ACC_TURB ((TFG_ACC) & 8)
+#ifndef TFG_QSUM_F64
+#define TFG_QSUM_F64 0
+#endif
+#define TFG_ACC_SUM (((TFG_ACC) & 16) || TFG_QSUM_F64)
+
 template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
                                       const tfg_uniforms& u, const double* __restrict__ geo_d, int64_t n_pad,
@@ -981,8 +1037,24 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   } else {
     inv_esat = 100.0f * fexp2((2353.0f * rT - 11.4f) * 3.3219280948873626f);
   }
+#if TFG_ACC_DEW
+  // e_air [mbar] (:809-826), the dew point (:888-893) and the surface
+  // temperature (:906-910) in fp64
+  const double e_d = (double)Hum_sp * (double)P_air * rcp_d(fma(p.one_minus_eps, (double)Hum_sp, p.eps)) * 0.01;
+  const float e_air = (float)e_d;
+  const double L_d = ln_d(e_d * (1.0 / 6.1121));
+  const double T_dew_d = 257.14 * L_d * rcp_d(18.678 - L_d);
+  const double T_surf_d = (snow_pos || ice_pos) ? dmin<NS>(T_dew_d, 0.0) : T_dew_d;
+  // only the fp32-rounded results live on (register pressure): each is then
+  // within 6e-8 of its fp64 value, where the fp32 chain was ~1e-6 K off
+  const float T_dew = (float)T_dew_d, T_surf = (float)T_surf_d;
+  const float dTs = (float)((double)T_air - T_surf_d);
+#if TFG_ACC_EM
+  const float em_root = (float)fma(p.one_minus_F_172 * p.cloud_term,
+                                   root7_d((e_d * 0.1) * rcp_d((double)T_air + 273.15)), p.F);
+#endif
+#else
   const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
-  const float RH = e_air * inv_esat;
   // dew point (:888-893) and surface temperature (:906-910)
   // ln(e_air / 6.1121) as the log of the ratio (~1): v_log_f32's mean error is
   // -0.44 ulp of its result, so a result near zero keeps that bias negligible,
@@ -999,14 +1071,30 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
 #endif
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
   const float T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
+#endif
+  const float RH = e_air * inv_esat;
   // turbulent fluxes (:640-745, :919-934)
+#if !TFG_ACC_DEW
   const float dTs = T_air - T_surf;
+#endif
+#if TFG_ACC_TURB
+  const double dTs_d = (double)dTs;
+  const double TK_d = (double)T_air + 273.15;
+  double bot_d = ((double)uz * (double)uz) * TK_d;
+  if (bot_d == 0.0) bot_d = 0.01;
+  const double Ri_d = p.gz * dTs_d * rcp_d(bot_d);
+  const double Ln_d = ln_d(dmax<NS>((p.z - st.h_snow) * p.inv_z0, 0.01));
+  const double Dn_d = (double)uz * (p.kappa * p.kappa) * rcp_d(Ln_d * Ln_d);
+  const double Dh_d = (Ri_d > 0.0) ? Dn_d * rcp_d(fma(10.0, Ri_d, 1.0)) : Dn_d * fma(-10.0, Ri_d, 1.0);
+  const float Dh = (float)Dh_d;
+#else
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
   const float Ri = p.f_gz * dTs * frcp(bot);
   const float L2 = flog2_split(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
   const float Dn = uz * p.f_k2 * frcp(L2 * L2);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
+#endif
   // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
   // (:853), written without the cancellation of the two near-equal pressures:
   //   e_air - e_surf = -e_air*expm1(x),  x = -k*dTs/((T_s+c)(T_a+c))
@@ -1024,7 +1112,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;  // k*log2(e)
   const float de = fmaf(-e_air, fexp2(xs2), e_air);
 #endif
+#if TFG_ACC_TURB
+  const float Qh = (float)(p.rho_air_Cp_air * Dh_d * dTs_d);
+#else
   const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
+#endif
   const float Qe = p.f_qe * Dh * de * fexp2(g.ek * rT);  // lhc / p0 folded
   // snowfall window + albedo ageing (:1006-1059)
   {
@@ -1088,14 +1180,30 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   } else {
     em_air = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
   }
+#if TFG_ACC_EM
+  // (e/T)^(1/7) from fp64 e_air and T_K, rounded to fp32 once (:1167)
+#if TFG_ACC_DEW
+  if (!p.satterlund) em_air = em_root;
+#else
+  if (!p.satterlund)
+    em_air = (float)fma(p.one_minus_F_172 * p.cloud_term,
+                        root7_d(((double)e_air * 0.1) * rcp_d((double)T_air + 273.15)), p.F);
+#endif
+#endif
+  const double em_d = (double)em_air;
+#if TFG_ACC_LW
+  const double TK_d2 = (double)T_air + 273.15, tks = (double)T_surf + 273.15;
+  const double a2 = TK_d2 * TK_d2, s2 = tks * tks;
+  const double Qn_LW_d = p.em_surf_sigma * fma(em_d, a2 * a2, -(s2 * s2));
+  const float Qn_LW = (float)Qn_LW_d;
+#else
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
-  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air, ta2 * ta2, -(ts2 * ts2));
-#ifndef TFG_QSUM_F64
-#define TFG_QSUM_F64 0
+  const float Qn_LW = p.f_em_surf_sigma * fmaf((float)em_d, ta2 * ta2, -(ts2 * ts2));
+  const double Qn_LW_d = (double)Qn_LW;
 #endif
-#if TFG_QSUM_F64  // the flux sum and E_in in fp64 (measurement switch)
-  double Q_sum = (((double)Qn_SW + (double)Qn_LW) + (double)Qh) + (double)Qe;
+#if TFG_ACC_SUM  // the flux sum and E_in in fp64
+  double Q_sum = (((double)Qn_SW + Qn_LW_d) + (double)Qh) + (double)Qe;
   if constexpr (QC) Q_sum = Q_sum + (double)qc;  // :1314, Qc last (Qa = 0)
 #else
   float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
@@ -1104,7 +1212,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
 
   melt_fast<NS>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
 #if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
-  const float dbg[13] = {(float)Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, Ri, L2, de, fexp2(g.ek * rT)};
+  const float dbg[13] = {(float)Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, 0.0f, 0.0f, de, fexp2(g.ek * rT)};
   o.RH = dbg[TFG_DEBUG_TERM];
 #endif
 #if defined(TFG_DEBUG_TERMS)  // diagnostic builds only (tests/diagnostics/term_attribution.py): the
