@@ -273,10 +273,13 @@ int tfg_sync(tfg_handle* h);
  * everything the launch reads (its forcing frames or tfg_update's inputs, the
  * elevation raster, the Qc plane in use, the state and the snowfall window) is
  * known to be finite, and its NaN-safe form otherwise; the results agree
- * wherever the data is finite.  Finiteness is checked where data enters
- * (tfg_set_field, tfg_set_inputs and tfg_update from host memory) and, for
- * launches of 8 or more steps, lazily before the launch (a synchronous device
- * check) where it is unknown.  *count = launches that ran the NaN-safe form.
+ * wherever the data is finite.  Finiteness is checked where data enters from
+ * host memory (tfg_set_field, tfg_set_inputs and tfg_update; fp64 values as
+ * the fp32 values they become).  Data set from device memory stays
+ * stream-ordered (no host wait) and of unknown status; before a launch of 8
+ * or more steps unknown data is checked (a synchronous device check), and a
+ * shorter launch runs the NaN-safe form.  *count = launches that ran the
+ * NaN-safe form.
  * The environment variable TFG_NANSAFE=1 at tfg_create forces that form. */
 int tfg_nan_safe_launches(tfg_handle* h, int64_t* count);
 

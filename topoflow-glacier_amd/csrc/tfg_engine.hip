@@ -1593,6 +1593,17 @@ int tfg_selftest_powers(int device, const double* x, int64_t n, int which, doubl
   return TFG_OK;
 }
 
+#ifdef TFG_WG_TIMING
+// diagnostic builds only: the last k_fused<float> launch's per-workgroup
+// [start, end, (xcc << 32) | cu] records (tfg_fused.hpp, g_wg_times)
+int tfg_debug_wg_times(unsigned long long* out, int n) {
+  if (!out || n < 0 || n > TFG_WG_TIMING) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  HIPCHK(nullptr, hipDeviceSynchronize());
+  HIPCHK(nullptr, hipMemcpyFromSymbol(out, HIP_SYMBOL(tfg_kern::g_wg_times), (size_t)n * 24));
+  return TFG_OK;
+}
+#endif
+
 int tfg_nan_safe_launches(tfg_handle* h, int64_t* count) {
   if (!h || !count) return fail(h, TFG_ERR_ARG, "null argument");
   *count = h->ns_launches;

@@ -206,6 +206,11 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_WG_PERM
 #define TFG_WG_PERM 0
 #endif
+#ifdef TFG_WG_TIMING  // diagnostic builds (tests/diagnostics/wg_timeline.py): for the first
+                      // TFG_WG_TIMING workgroups of every k_fused launch, the wall clock
+                      // (100 MHz) at start and end and the XCC / CU it ran on
+static __device__ unsigned long long g_wg_times[TFG_WG_TIMING][3];
+#endif
 #ifndef TFG_START_STAGGER
 #define TFG_START_STAGGER 0
 #endif
@@ -230,6 +235,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
                                                   double* __restrict__ slab,       // [gridDim][n_catch][6]
                                                   const R* __restrict__ qcf) {     // [n_pad] Qc [W m-2] (QC) | null
   extern __shared__ double lds_bins[];  // [kWaves][n_catch][6]
+#ifdef TFG_WG_TIMING
+  const unsigned long long t_wg0 = wall_clock64();
+#endif
   const DevParams& p = a.p;
   const int nb = a.n_catch * 6;
   for (int i = threadIdx.x; i < kWaves * nb; i += kBlock) lds_bins[i] = ((i % 6) == 5) ? -INFINITY : 0.0;
@@ -555,6 +563,15 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       bslab[i] += v;
     }
   }
+#ifdef TFG_WG_TIMING
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x < TFG_WG_TIMING) {
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
+    g_wg_times[blockIdx.x][0] = t_wg0;
+    g_wg_times[blockIdx.x][1] = wall_clock64();
+    g_wg_times[blockIdx.x][2] = ((unsigned long long)xcc << 32) | (unsigned)__smid();
+  }
+#endif
   if (a.io_flag) {  // tfg_update: tell the waiting host this workgroup is done
     __threadfence_system();
     __syncthreads();

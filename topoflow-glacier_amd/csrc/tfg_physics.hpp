@@ -955,9 +955,10 @@ __device__ __forceinline__ void melt_fast(const DevParams& p, QS Q_sum, float P_
 
 // fp64 pieces for the fp32 engine's accuracy promotions (TFG_ACC, below).
 // rcp_d: 1/x from v_rcp_f32 and one fp64 Newton step (relative error ~1e-14;
-// x within fp32 range).  ln_d: ln x to ~1e-15 relative for finite x > 0
-// (x = 2^e m, m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh((m-1)/(m+1)) as an odd
-// series to t^11, |t| <= 0.172), the hardware log for 0, inf and NaN (their
+// x within fp32 range).  ln_d: ln x within 2e-11 for finite x > 0 (x = 2^e m,
+// m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh((m-1)/(m+1)) as an odd series to
+// t^11, |t| <= 0.172; 100x below what the fp32 engine's tolerance needs of the
+// dew point and the roughness log), the hardware log for 0, inf and NaN (their
 // numpy values: -inf, inf, NaN).  root7_d: x^(1/7) from the fp32 power and one
 // Newton step (relative error ~1e-13).
 __device__ __forceinline__ double rcp_d(double x) {
