@@ -342,10 +342,10 @@ def sample_parity(args, plan: dict, world: int, rank: int, local: int, threads: 
                  "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on {n} cells x {steps} steps "
                            f"({t_np:.1f} s), the reference of the parity check"}
     c64, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=frames, hist=True, nthreads=threads)
-    flip64, genuine64 = melt_out_flips({v: c64[v] for v in HIST}, ref)
-    flip, genuine = melt_out_flips(gpu, ref)
-    ok = valid_mask(flip, steps)
     tol = 1e-5 if args.engine == "float32" else 1e-10
+    flip64, genuine64 = melt_out_flips({v: c64[v] for v in HIST}, ref, tol)
+    flip, genuine = melt_out_flips(gpu, ref, tol)
+    ok = valid_mask(flip, steps)
     by_out = {v: _floored_rel(gpu[v][ok], ref[v][ok])[0] for v in HIST}
     err = max(by_out.values())
     pure = {}  # the fraction of compared values above pure-relative 1e-5

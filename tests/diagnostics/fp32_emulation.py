@@ -20,7 +20,7 @@ log biased by -0.44 ulp), and its miss rates are a lower bound of the GPU's.
   "wb"    the snowfall cold content in fp64
   "all"   every flux in fp64
 
-  python tests/diagnostics/fp32_emulation.py [cells] [steps] [variant,variant,...]
+  python tests/diagnostics/fp32_emulation.py [cells] [steps] [variant,variant,...] [out.json]
 prints, per variant, the fraction of cell-steps beyond pure-relative 1e-5 of
 the numpy oracle (cells with a melt-out flip compared up to the flip, as
 bench.py's parity check does).
@@ -344,6 +344,9 @@ def main():
         res["s"] = round(time.time() - t0, 1)
         out[var or "fp32"] = res
         print(var or "fp32", json.dumps(res), flush=True)
+    if len(sys.argv) > 4:
+        Path(sys.argv[4]).write_text(json.dumps({"cells": n, "steps": steps, "unit": "% of compared cell-steps beyond "
+                                                 "pure-relative 1e-5 of the numpy oracle", "variants": out}, indent=1) + "\n")
     return out
 
 

@@ -546,6 +546,15 @@ __global__ void k_nonfinite(const T* __restrict__ p, int64_t n, int64_t stride, 
       bad |= !isfinite(p[k * stride + i]);
   if (bad) atomicOr(flag, 1);
 }
+// the same check for each of a frame's planes at once (blockIdx.y = plane): flags[plane] |= 1
+template <class T>
+__global__ void k_nonfinite_planes(const T* __restrict__ p, int64_t n, int64_t stride, int32_t* __restrict__ flags) {
+  const T* __restrict__ q = p + (int64_t)blockIdx.y * stride;
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(q[i]);
+  if (bad) atomicOr(flags + blockIdx.y, 1);
+}
 __global__ void k_window_nan(const int64_t* __restrict__ tot, int64_t n, int32_t* __restrict__ flag) {
   bool bad = false;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -650,6 +659,7 @@ struct tfg_handle {
   // is known to be finite.  kUnknown: written by a path that did not check it;
   // kDirty: checked, holds a NaN or an infinity.
   std::vector<uint8_t> plane_state;  // [n_frames][kNumForc] forcing planes
+  std::vector<int> chk_frames;       // choose_form's scratch list of frames to check
   uint8_t state_state = 1;           // fp64 state planes and the snowfall window
   uint8_t elev_state = 1;            // the elevation raster (the fp32 flux reads it unguarded)
   uint8_t qc_state = 1;              // the Qc plane while the conduction term is on
@@ -1079,7 +1089,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {&h->hist, (size_t)hist_depth * kNumHist * np * rs},
       {(void**)&h->diag, (size_t)n_catch * 6 * 8},
       {(void**)&h->slab, (size_t)h->max_blocks * n_catch * 6 * 8},
-      {(void**)&h->d_flag, 4},
+      {(void**)&h->d_flag, (size_t)n_frames * kNumForc * 4},  // a flag per forcing plane (choose_form)
   };
   // TFG_ARENA=1 (measurement switch): the streamed planes -- forcing frames,
   // window slots and output slots -- in one allocation, so that their
@@ -1451,15 +1461,40 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
   if (io.in) {
     inputs_ok = io.in_state == kOk;
   } else {
-    for (int k = 0; k < K; ++k) {
-      uint8_t* ps = &h->plane_state[(size_t)u[k].frame * kNumForc];
-      for (int f = 0; f < kNumForc; ++f) {
-        if (ps[f] == kUnknown && check) {
-          char* plane = static_cast<char*>(h->forc) + ((size_t)u[k].frame * kNumForc + f) * h->n_pad * h->rsz;
-          if (int rc = check_finite(h, plane, h->engine, h->n, &ps[f])) return rc;
-        }
-        inputs_ok &= ps[f] == kOk;
+    if (check) {
+      // every frame the launch reads that holds a plane of unknown status is
+      // checked on the device, all of them before one host wait
+      int nf = 0;
+      for (int k = 0; k < K; ++k) {
+        const int fr = u[k].frame;
+        const uint8_t* ps = &h->plane_state[(size_t)fr * kNumForc];
+        if (std::find(ps, ps + kNumForc, kUnknown) == ps + kNumForc) continue;
+        if (std::find(h->chk_frames.begin(), h->chk_frames.begin() + nf, fr) != h->chk_frames.begin() + nf) continue;
+        if ((int)h->chk_frames.size() <= nf) h->chk_frames.resize(nf + 1);
+        h->chk_frames[nf++] = fr;
       }
+      if (nf) {
+        HIPCHK(h, hipMemsetAsync(h->d_flag, 0, (size_t)nf * kNumForc * 4, h->stream));
+        const dim3 grid(std::max(1, std::min(grid_for(h->n), 2048)), kNumForc);
+        for (int j = 0; j < nf; ++j) {
+          const char* fp = static_cast<const char*>(h->forc) + (size_t)h->chk_frames[j] * kNumForc * h->n_pad * h->rsz;
+          hipLaunchKernelGGL((k_nonfinite_planes<float>), grid, 256, 0, h->stream, (const float*)fp, h->n, h->n_pad,
+                             h->d_flag + j * kNumForc);
+        }
+        HIPCHK(h, hipGetLastError());
+        std::vector<int32_t> flags((size_t)nf * kNumForc);
+        HIPCHK(h, hipMemcpyAsync(flags.data(), h->d_flag, flags.size() * 4, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        for (int j = 0; j < nf; ++j) {
+          uint8_t* ps = &h->plane_state[(size_t)h->chk_frames[j] * kNumForc];
+          for (int f = 0; f < kNumForc; ++f)
+            if (ps[f] == kUnknown) ps[f] = flags[(size_t)j * kNumForc + f] ? kDirty : kOk;
+        }
+      }
+    }
+    for (int k = 0; k < K; ++k) {
+      const uint8_t* ps = &h->plane_state[(size_t)u[k].frame * kNumForc];
+      for (int f = 0; f < kNumForc; ++f) inputs_ok &= ps[f] == kOk;
     }
   }
   if (check && (h->state_state == kUnknown || (h->state_state == kDirty && --h->state_recheck <= 0))) {
