@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 tag=${TAG:-r4b}
 i=0
-for v in ${VARIANTS:-base acc1 acc5 base acc3 acc7 acc23 base}; do
+for v in ${VARIANTS:-base acc1 acc7 acc23 base acc15 acc31 base}; do
   i=$((i+1))
   lib=topoflow-glacier_amd/topoflow_glacier/_tfg.so
   [ "$v" = base ] || lib=diag_libs/_tfg_$v.so

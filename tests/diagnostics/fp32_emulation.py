@@ -168,11 +168,20 @@ class Fp32Engine:
             T_surf = np.where(snow_pos | ice_pos, np.minimum(T_dew, f32(0)), T_dew)
             dTs = T_air - T_surf
             T_surf64, dTs64 = f64(T_surf), f64(dTs)
-        if "turb" in pr or "turbc" in pr:
+        if "turb" in pr or "turbc" in pr or "turbn" in pr or "turbs" in pr:
             bot = f64(uz) ** 2 * (f64(T_air) + 273.15)
             bot = np.where(bot == 0, 0.01, bot)
             Ri = c["g"] * 10.0 * dTs64 / bot
-            ln = np.log if "turb" in pr else ln_c
+            if "turbs" in pr:  # fp32 log2 y of the fp32-rounded argument, its Newton correction c in fp32, y + c in fp64
+                def ln(a):
+                    af = np.asarray(a, f64).astype(f32)
+                    y = log2_32(af)
+                    cc = fma32(af, exp2_32(-y), f32(-1.0)) * LOG2E
+                    return (f64(y) + f64(cc)) * np.log(2.0)
+            elif "turbn" in pr:  # the fp32 Newton-refined log2 of the fp32-rounded argument
+                ln = lambda a: f64(log2_nr(np.asarray(a, f64).astype(f32))) * np.log(2.0)  # noqa: E731
+            else:
+                ln = np.log if "turb" in pr else ln_c
             arg = c["kappa"] / ln(np.maximum((10.0 - self.h_snow) / c["z0_air"], 0.01))
             Dn = f64(uz) * arg * arg
             Dh64 = np.where(Ri > 0, Dn / (1 + 10 * Ri), Dn * (1 - 10 * Ri))

@@ -996,7 +996,7 @@ __device__ __forceinline__ double root7_d(double x) {
 //            and their difference (LW_in ~ LW_out ~ 300 W m-2 cancel to ~100)
 //   2  DEW   e_air, the dew point, T_surf and T_air - T_surf (:809-911)
 //   4  EM    em_air's (e/T)^(1/7) (:1167)
-//   8  TURB  Ri, Dn, Dh and Qh (:626-745)
+//   8  TURB  Ri, Dn, Dh and Qh (:626-745), the roughness log as fp32 + correction
 //  16  SUM   the flux sum and E_in (:1259-1319, :1364)
 #ifndef TFG_ACC
 #define TFG_ACC 0
@@ -1084,7 +1084,13 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   double bot_d = ((double)uz * (double)uz) * TK_d;
   if (bot_d == 0.0) bot_d = 0.01;
   const double Ri_d = p.gz * dTs_d * rcp_d(bot_d);
-  const double Ln_d = ln_d(dmax<NS>((p.z - st.h_snow) * p.inv_z0, 0.01));
+  // ln((z - h_snow)/z0) ~ 9: only its relative error reaches Dn, so the fp32
+  // log2 y of the fp32-rounded argument plus its Newton correction c, added
+  // in fp64 (y alone, an fp32 number near 13, is 3.6e-8 off at best)
+  const float la = (float)dmax<NS>((p.z - st.h_snow) * p.inv_z0, 0.01);
+  const float ly = flog2(la);
+  const float lc = fmaf(la, fexp2(-ly), -1.0f) * kLog2e;
+  const double Ln_d = ((double)ly + (double)lc) * 0.69314718055994531;
   const double Dn_d = (double)uz * (p.kappa * p.kappa) * rcp_d(Ln_d * Ln_d);
   const double Dh_d = (Ri_d > 0.0) ? Dn_d * rcp_d(fma(10.0, Ri_d, 1.0)) : Dn_d * fma(-10.0, Ri_d, 1.0);
   const float Dh = (float)Dh_d;
