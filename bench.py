@@ -423,22 +423,25 @@ def shard_plan(args, world: int, rank: int) -> dict:
 
 def pmc_traffic(rows, args):
     """HBM bytes per launch from the committed PMC profile of this shard shape
-    (scripts/gpu_pmc.sh -> profiles/pmc_<nx>x<rows>_fuse<K>.json), quoted only
-    when the profile was measured on the same machine code of the timed kernel
-    as the running library's (_native.kernel_code_sha256: the kernel's
-    instructions, descriptor and callees, not the other kernels of the
-    library); otherwise null, with the reason."""
+    and engine (scripts/gpu_pmc.sh -> profiles/pmc_<nx>x<rows>_fuse<K>.json for
+    the fp32 engine, ..._f64.json for the fp64 one), quoted only when the
+    profile was measured on the same machine code of the timed kernel as the
+    running library's (_native.kernel_code_sha256: the kernel's instructions,
+    descriptor and callees, not the other kernels of the library); otherwise
+    null, with the reason."""
     from topoflow_glacier import _native as nat
 
-    pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}.json"
-    running = nat.kernel_code_sha256()
-    if args.engine != "float32" or args.catchments or args.dt != 1.0 or args.conduction:
+    suffix = "" if args.engine == "float32" else "_f64"
+    symbol = nat.BENCH_KERNEL if args.engine == "float32" else nat.BENCH_KERNEL_F64
+    pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}{suffix}.json"
+    if args.catchments or args.dt != 1.0 or args.conduction:
         return None, {"profile": None, "reason": "no PMC profile for this variant of the kernel"}
     if not pmc.exists():
         return None, {"profile": None, "reason": f"{pmc.relative_to(ROOT)} not measured"}
+    running = nat.kernel_code_sha256(symbol)
     prof = json.loads(pmc.read_text())
     measured = prof.get("kernel_code_sha256")
-    src = {"profile": str(pmc.relative_to(ROOT)), "kernel": nat.BENCH_KERNEL, "kernel_code_sha256": measured,
+    src = {"profile": str(pmc.relative_to(ROOT)), "kernel": symbol, "kernel_code_sha256": measured,
            "running_kernel_code_sha256": running, "match": measured is not None and measured == running,
            "read_scale": corr.get("read_scale") if isinstance(corr := prof.get("correction"), dict) else None}
     return (prof.get("hbm_bytes_per_launch") if src["match"] else None), src

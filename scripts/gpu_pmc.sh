@@ -5,8 +5,9 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${PMC_TAG:-pmc}
 mkdir -p $OUT
-# every k_fused dispatch of this run is a full 128-step launch (warm-up included)
-ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --fuse 128 --steps 128 --warmup 128 --no-cpu-baseline --no-pcie}"
+# every k_fused dispatch of this run is a full 128-step launch (warm-up included;
+# no parity or drop-in legs, whose launches would enter the per-dispatch means)
+ARGS="${PMC_ARGS:---ny 8192 --nx 8192 --fuse 128 --steps 768 --warmup 128 --no-cpu-baseline --no-dropin --no-parity}"
 i=0
 while IFS= read -r line; do
   [ -z "$line" ] && continue
@@ -25,4 +26,4 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "calibration $c rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $d.log; exit $rc; fi
 done
-python3 scripts/pmc_profile.py $OUT ${PMC_PROFILE:-$OUT/profile.json} ${PMC_SHAPE:-8192 8192 128} 67108864 8
+python3 scripts/pmc_profile.py $OUT ${PMC_PROFILE:-$OUT/profile.json} ${PMC_SHAPE:-8192 8192 128} 67108864 8 ${PMC_ENGINE:-float32}

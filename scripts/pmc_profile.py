@@ -1,7 +1,13 @@
 """Turn the rocprofv3 --pmc passes of scripts/gpu_pmc.sh into the traffic
 profile bench.py quotes (profiles/pmc_<nx>x<ny>_fuse<K>.json).
 
-  python3 scripts/pmc_profile.py <pmc dir> <out json> [nx ny fuse]
+  python3 scripts/pmc_profile.py <pmc dir> <out json> [nx ny fuse [cal cells, cal steps [engine]]]
+
+engine float32 (default): k_fused<float, false, false, false, false, 1, false>,
+4-byte lanes.  engine float64: k_fused<double, true, false, false, false, 1,
+false>, whose forcing, geometry, state and output planes are 8-byte lanes and
+whose window slots are 4-byte lanes; each counter is corrected per lane width,
+weighted by the algorithmic bytes of each width (bench.bytes_model).
 
 * k_fused passes: <dir>/p*/run_counter_collection.csv (one counter set each).
 * Calibration passes: <dir>/cal_fetch, <dir>/cal_write (tools/hbm_mix ... cal):
@@ -25,7 +31,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "topoflow-glacier_amd"))
-from topoflow_glacier._native import code_object_sha256, kernel_code_sha256  # noqa: E402
+from topoflow_glacier import _native as nat  # noqa: E402
 
 sys.path.insert(0, str(ROOT))
 from bench import launch_bytes_per_cell  # noqa: E402  
@@ -51,6 +57,8 @@ def calibration(d: Path, cells: int, steps: int):
     kernels = {  # tools/hbm_mix.hip k_mix<R, W, V, NT>
         "read only 4 B/lane": ("k_mix<7, 0, 1, false>", "FETCH_SIZE", 7),
         "read only 16 B/lane": ("k_mix<7, 0, 4, false>", "FETCH_SIZE", 7),
+        "read only 8 B/lane": ("k_mix<7, 0, 2, false>", "FETCH_SIZE", 7),
+        "write only 8 B/lane nt": ("k_mix<0, 7, 2, true>", "WRITE_SIZE", 7),
         "write only 4 B/lane": ("k_mix<0, 7, 1, false>", "WRITE_SIZE", 7),
         "write only 4 B/lane nt": ("k_mix<0, 7, 1, true>", "WRITE_SIZE", 7),
         "k_fused mix reads 4 B/lane nt": ("k_mix<6, 7, 1, true>", "FETCH_SIZE", 6),
@@ -68,29 +76,61 @@ def calibration(d: Path, cells: int, steps: int):
     return out
 
 
+KERNELS = {  # engine -> (rocprofv3 kernel-name match, _native symbol prefix, description)
+    "float32": ("k_fused<float, false, false", "BENCH_KERNEL", "k_fused<float,false,false,false,false,1,false> (fp32 engine, clean form"),
+    "float64": ("k_fused<double, true, false, false, false", "BENCH_KERNEL_F64",
+                "k_fused<double,true,false,false,false,1,false> (fp64 engine"),
+}
+
+
+def scale_of(cal, name, default):
+    return 1.0 / cal[name]["counter_over_known"] if name in cal else default
+
+
 def main():
     d, out = Path(sys.argv[1]), Path(sys.argv[2])
     nx, ny, fuse = (int(x) for x in sys.argv[3:6]) if len(sys.argv) > 5 else (8192, 8192, 96)
-    raw = per_dispatch(sorted(glob.glob(str(d / "p*" / "run_counter_collection.csv"))), "k_fused<float, false, false")
+    engine = sys.argv[8] if len(sys.argv) > 8 else "float32"
+    match, sym, desc = KERNELS[engine]
+    raw = per_dispatch(sorted(glob.glob(str(d / "p*" / "run_counter_collection.csv"))), match)
     cal = calibration(d, cells=int(sys.argv[6]) if len(sys.argv) > 6 else 67108864,
                       steps=int(sys.argv[7]) if len(sys.argv) > 7 else 8)
-    rd_scale = 1.0 / cal["read only 4 B/lane"]["counter_over_known"] if "read only 4 B/lane" in cal else 2.0
-    wr_scale = 1.0 / cal["write only 4 B/lane nt"]["counter_over_known"] if "write only 4 B/lane nt" in cal else 1.0
+    rd4 = scale_of(cal, "read only 4 B/lane", 2.0)
+    wr4 = scale_of(cal, "write only 4 B/lane nt", 1.0)
+    if engine == "float32":
+        rd_scale, wr_scale = rd4, wr4
+        elem = 4
+    else:
+        # bytes by lane width per cell and launch (bench.bytes_model, elem 8):
+        # reads: forcing 5x8 per step + geometry 7x8 + state 7x8 (8 B lanes),
+        # window slot 4 per step (4 B); writes: outputs 6x8 per step + state
+        # 7x8 (8 B), window slot 4 per step (4 B)
+        elem = 8
+        rd8, wr8 = scale_of(cal, "read only 8 B/lane", rd4), scale_of(cal, "write only 8 B/lane nt", wr4)
+        r8, r4 = 40 * fuse + 56 + 56, 4 * fuse
+        w8, w4 = 48 * fuse + 56, 4 * fuse
+        rd_scale = (r8 + r4) / (r8 / rd8 + r4 / rd4)
+        wr_scale = (w8 + w4) / (w8 / wr8 + w4 / wr4)
     rd = raw["FETCH_SIZE"] * 1024 * rd_scale
     wr = raw["WRITE_SIZE"] * 1024 * wr_scale
-    alg = nx * ny * launch_bytes_per_cell(fuse)
+    alg = nx * ny * launch_bytes_per_cell(fuse, elem)
+    symbol = getattr(nat, sym)
     res = {
-        "kernel": f"k_fused<float,false,false,false,false,1,false> (fp32 engine, clean form, {fuse} steps fused) at {nx}x{ny}",
+        "kernel": f"{desc}, {fuse} steps fused) at {nx}x{ny}",
+        "engine": engine,
         "command": "bash scripts/gpu_pmc.sh (rocprofv3 --pmc <pass> -- python3 bench.py ...; one counter set per pass; "
                    "calibration: rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE -- tools/hbm_mix 67108864 8 2048 0 cal); "
                    "python3 scripts/pmc_profile.py",
-        "kernel_code_sha256": kernel_code_sha256(),
-        "code_object_sha256": code_object_sha256(),
+        "kernel_symbol": symbol,
+        "kernel_code_sha256": nat.kernel_code_sha256(symbol),
+        "code_object_sha256": nat.code_object_sha256(),
         "correction": {
             "read_scale": rd_scale, "write_scale": wr_scale,
             "source": "measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch. FETCH_SIZE "
                       "reports half the streamed read bytes at 4 B lanes (k_fused's width) as at 16 B lanes (the "
-                      "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes",
+                      "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes"
+                      + ("" if engine == "float32" else "; fp64 engine: the 8 B and 4 B lane scales weighted by "
+                         "the algorithmic bytes of each width"),
             "calibration": cal,
         },
         "hbm_read_bytes_per_launch": rd,

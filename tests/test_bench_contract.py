@@ -69,6 +69,27 @@ def test_byte_model_prices_each_engine_by_its_element_size():
     assert bench.bytes_model(4, catchments=True, qc=True) == (52, 132 + 4 + 4)
 
 
+def test_pmc_traffic_is_keyed_by_engine_and_kernel_code(tmp_path, monkeypatch):
+    """roofline.traffic comes from the engine's own PMC profile (_f64 suffix for
+    the fp64 engine), and only when the profile's kernel hash equals the
+    running library's hash of that engine's timed kernel."""
+    bench, args = _args("--ny", "4096", "--nx", "4096", "--engine", "float64", "--fuse", "192")
+    from topoflow_glacier import _native as nat
+
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    (tmp_path / "profiles").mkdir()
+    prof = tmp_path / "profiles" / "pmc_4096x4096_fuse192_f64.json"
+    t, src = bench.pmc_traffic(4096, args)
+    assert t is None and "not measured" in src["reason"]
+    monkeypatch.setattr(nat, "kernel_code_sha256", lambda sym=nat.BENCH_KERNEL, path=None: "h-" + sym)
+    prof.write_text(json.dumps({"kernel_code_sha256": "h-" + nat.BENCH_KERNEL_F64, "hbm_bytes_per_launch": 1.5e12}))
+    t, src = bench.pmc_traffic(4096, args)
+    assert t == 1.5e12 and src["match"] and src["kernel"] == nat.BENCH_KERNEL_F64
+    prof.write_text(json.dumps({"kernel_code_sha256": "h-" + nat.BENCH_KERNEL, "hbm_bytes_per_launch": 1.5e12}))
+    t, src = bench.pmc_traffic(4096, args)  # an fp32 kernel's profile is not quoted for the fp64 engine
+    assert t is None and not src["match"]
+
+
 def test_config5_eight_gpu_command_fits_its_shards():
     """BASELINE config 5 as the driver would run it on 8 GPUs
     (`--gpus 8 --ny 16384 --nx 16384 --dt 0.25 --catchments 43`): 2048 x 16384

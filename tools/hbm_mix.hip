@@ -333,6 +333,8 @@ int main(int argc, char** argv) {
     // (k_fused's width) against 16 B lanes (the guide's calibration).
     run<7, 0>("cal read only 4 B/lane", in, out, n, steps, frames);
     run<7, 0, 4>("cal read only 16 B/lane", in, out, n, steps, frames);
+    run<7, 0, 2>("cal read only 8 B/lane", in, out, n, steps, frames);  // the fp64 engine's width
+    run<0, 7, 2, true>("cal write only 8 B/lane nt", in, out, n, steps, frames);
     run<0, 7>("cal write only 4 B/lane", in, out, n, steps, frames);
     run<0, 7, 1, true>("cal write only 4 B/lane nt", in, out, n, steps, frames);
     run<6, 7, 1, true>("cal k_fused mix 4 B/lane nt", in, out, n, steps, frames);

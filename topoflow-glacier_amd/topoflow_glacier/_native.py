@@ -167,6 +167,7 @@ def code_object_sha256(path: Path | None = None) -> str | None:
 
 
 BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0E"  # k_fused<float, false, false, false, false, 1, false>
+BENCH_KERNEL_F64 = "_ZN8tfg_kern7k_fusedIdLb1ELb0ELb0ELb0ELi1ELb0E"  # k_fused<double, true, false, false, false, 1, false>
 
 
 def gfx950_code_objects(path: Path | None = None) -> list[bytes]:
