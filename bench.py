@@ -196,6 +196,10 @@ def parse():
     ap.add_argument("--no-parity", action="store_true", help="skip the per-rank GPU-vs-oracle check")
     ap.add_argument("--no-dropin", action="store_true",
                     help="skip the drop-in path legs (per-step update() from device inputs, defer_update instances)")
+    ap.add_argument("--dropin-queued", action="store_true",
+                    help="add the queued variant of the per-step grid leg (the same steps set into frames, then one "
+                         "fused launch); off by default: its short launches of the timed kernel would enter the "
+                         "kernel's rocprof average")
     ap.add_argument("--dropin-instances", type=int, default=4096,
                     help="single-catchment BMI models of the defer_update leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -266,29 +270,82 @@ def _static_of(syn: dict) -> dict:
 
 def parity_plan(args, plan: dict, world: int) -> dict:
     """The cells and launches of a rank's parity check: whole rows at the top of
-    its OWN shard (global rows row0 .. row0 + rows - 1), and a one-step lead-in
-    launch (the k_fused instance that reads the initial depths) followed by one
-    whole launch of the timed depth, so that the timed kernel instance runs at
-    the timed launch length (at K = 128 the three-register-set step loop ends in
-    its two-step tail)."""
+    its OWN shard (global rows row0 .. row0 + rows - 1), read from the bench's
+    own handle, whose first launches are a one-step lead-in (the k_fused
+    instance that reads the initial depths) and then one whole launch of the
+    timed depth over the whole shard (capture_parity): the timed kernel
+    instance at the timed launch length and shape (at K = 128 the
+    three-register-set step loop ends in its two-step tail)."""
     want = args.parity_cells or (262144 if world == 1 else 65536)
     rows = max(1, min(plan["rows"], want // args.nx))
     k = args.parity_steps or args.fuse
     return {"row0": plan["row0"], "rows": rows, "cells": rows * args.nx, "launch_steps": [1, k], "steps": 1 + k}
 
 
-def sample_parity(args, plan: dict, world: int, rank: int, local: int, threads: int):
+def capture_parity(eng, args, plan: dict, world: int, torch, local: int) -> dict:
+    """The GPU side of this rank's parity check, on the bench's own handle
+    before its warm-up: a one-step lead-in launch, then ONE whole launch of
+    the timed depth over the whole shard, the same kernel instance and launch
+    shape as every timed launch.  Keeps the outputs of the first parity_plan
+    cells (a leading block of rows; tfg_get_field reads that prefix) at all
+    1 + K steps, and the shard's mass-balance integrals after these steps
+    beside fp64 sums of the forcing frames they read (torch on the device,
+    per catchment: vol_P, vol_PR, vol_PS, P_max; :558-624)."""
+    pp = parity_plan(args, plan, world)
+    n, k = pp["cells"], pp["launch_steps"][1]
+    if eng.step_index != 0 or k > eng.hist_depth:
+        raise RuntimeError("capture_parity runs first on the handle, and keeps at most hist_depth steps")
+    ns0 = eng.nan_safe_launches() if args.engine == "float32" else 0
+    eng.run(1)  # lead-in: hist slot 0
+    eng.sync()
+    gpu = {v: [eng.get_field(v, index=0, dtype=np.float32 if args.engine == "float32" else np.float64, cells=n)]
+           for v in HIST}
+    eng.run(k)  # step j (1..k) writes slot j % hist_depth
+    eng.sync()
+    for v in HIST:
+        gpu[v] += [eng.get_field(v, index=j % eng.hist_depth, dtype=gpu[v][0].dtype, cells=n) for j in range(1, k + 1)]
+    gpu = {v: np.stack(x).astype(np.float64) for v, x in gpu.items()}
+    ns = (eng.nan_safe_launches() - ns0) if args.engine == "float32" else 0
+    diag = eng.diagnostics()
+    # what the shard's integrals must be: per-cell fp64 sums of the frames the 1 + k steps read
+    kc = max(args.catchments, 1)
+    dev = torch.device("cuda", local)
+    cnt = np.bincount(np.arange(1 + k) % args.frames, minlength=args.frames)
+    cid = torch.from_numpy(catchment_blocks(plan["row0"], plan["rows"], plan["ny_global"], args.nx, args.catchments)
+                           if args.catchments else np.zeros(eng.n, np.int32)).to(dev).long()
+    P = torch.empty(eng.n, dtype=torch.float32 if args.engine == "float32" else torch.float64, device=dev)
+    T = torch.empty_like(P)
+    sums = torch.zeros((3, eng.n), dtype=torch.float64, device=dev)
+    pmax = torch.full((kc,), -float("inf"), dtype=torch.float64, device=dev)
+    t_rs = BASE_CFG["T_rain_snow"]
+    for f in np.nonzero(cnt)[0]:
+        eng.get_field_device("P", P, index=int(f))
+        eng.get_field_device("T_air", T, index=int(f))
+        p64 = P.double()
+        rain = T.double() > t_rs
+        sums[0] += p64 * float(cnt[f])
+        sums[1] += torch.where(rain, p64, 0.0) * float(cnt[f])
+        sums[2] += torch.where(rain, 0.0, p64) * float(cnt[f])
+        pmax = pmax.scatter_reduce(0, cid, p64, reduce="amax", include_self=True)
+    da_dt = BASE_CFG["da"] * 1e6 * args.dt
+    want = torch.stack([torch.zeros(kc, dtype=torch.float64, device=dev).index_add_(0, cid, sums[i])
+                        for i in range(3)], 1).cpu().numpy() * da_dt
+    return {"plan": pp, "gpu": gpu, "nan_safe_launches": ns, "diag": diag, "want_P_PR_PS": want,
+            "want_P_max": pmax.cpu().numpy()}
+
+
+def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: dict):
     """This rank's GPU-vs-oracle check, outside the timed region (every rank,
-    at every N): the engine (same variant as the timed one: engine type, dt,
-    catchments, launch depth) on the first rows of this rank's shard, against
-    the numpy oracle (oracle/tfg_oracle.py, fp64, bit-exact to the reference
-    fixtures) on the host mirror of the same synthetic fp32 inputs, every
-    output at every step.  Cells whose trajectories part at a melt-out residual
-    are compared up to the flip and counted, held to the fp64 baseline of the
-    same cells and steps (the C oracle against the numpy oracle;
-    tests/harness.py flip_rule).  With catchments, the engine's per-catchment
-    precipitation integrals and P_max are checked against bincounts of the
-    forcing, and its melt integrals reported against the oracle's.
+    at every N): the outputs capture_parity kept from the bench handle's own
+    lead-in and first whole launch, on the first rows of this rank's shard,
+    against the numpy oracle (oracle/tfg_oracle.py, fp64, bit-exact to the
+    reference fixtures) on the host mirror of the same synthetic fp32 inputs,
+    every output at every step.  Cells whose trajectories part at a melt-out
+    residual are compared up to the flip and counted, held to the fp64
+    baseline of the same cells and steps (the C oracle against the numpy
+    oracle; tests/harness.py flip_rule).  The shard's per-catchment
+    precipitation integrals and P_max are checked against the sums of the
+    forcing it read.
 
     Returns (parity dict, the numpy run's single-core rate as a CPU leg)."""
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -296,32 +353,12 @@ def sample_parity(args, plan: dict, world: int, rank: int, local: int, threads: 
     import tfg_oracle_c as OC
 
     from tests.harness import flip_rule, melt_out_flips, valid_mask
-    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
-    from topoflow_glacier.engine import GlacierEngine
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
-    pp = parity_plan(args, plan, world)
+    pp = cap["plan"]
     rows, nx, row0, steps = pp["rows"], args.nx, pp["row0"], pp["steps"]
     n = pp["cells"]
-    n_catch = args.catchments + 1 if args.catchments > 0 else 1
-    cid = (catchment_blocks(row0, rows, plan["ny_global"], nx, args.catchments) if args.catchments
-           else np.zeros(n, np.int32))
-    # (1) the GPU: the same engine variant as the timed one
-    scfg = TopoflowGlacierConfig.model_validate(dict(BASE_CFG, ny=rows, nx=nx, dt=args.dt))
-    e = GlacierEngine(scfg, rows, nx, engine=args.engine, device=local, n_frames=args.frames, hist_depth=steps,
-                      fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
-    try:
-        e.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=nx)
-        if args.catchments:
-            e.set_field("catch_id", cid)
-        for k in pp["launch_steps"]:
-            e.run(k)
-        e.sync()
-        gpu = {v: np.stack([e.get_field(v, index=j) for j in range(steps)]) for v in HIST}
-        diag = e.diagnostics()
-        ns = e.nan_safe_launches() if args.engine == "float32" else 0
-    finally:
-        e.close()
+    gpu, diag, ns = cap["gpu"], cap["diag"], cap["nan_safe_launches"]
     # (2) the numpy oracle on the host mirror of the same inputs (global cell indices)
     cells = ((row0 + np.arange(rows))[:, None] * nx + np.arange(nx)[None, :]).reshape(-1)
     syn = synthetic_cells(args.seed, cells, diurnal_table(args.frames))
@@ -355,30 +392,22 @@ def sample_parity(args, plan: dict, world: int, rank: int, local: int, threads: 
             rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
         pure[v] = float(np.mean(rel > 1e-5))
     rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
-    # the mass-balance integrals of the same launches (:558-624, :1482-1494), per catchment
+    # the shard's mass-balance integrals after the same steps (:558-624), per catchment
     kc = max(args.catchments, 1)
-    da_dt = BASE_CFG["da"] * 1e6 * args.dt
-    Pk = forcing["P"][frames]
-    rain = forcing["T_air"][frames] > BASE_CFG["T_rain_snow"]
-    want = np.stack([np.bincount(cid, weights=w, minlength=kc)[:kc] * da_dt
-                     for w in (Pk.sum(0), np.where(rain, Pk, 0.0).sum(0), np.where(rain, 0.0, Pk).sum(0))], axis=1)
-    pmax = np.array([Pk[:, cid == c].max() if np.any(cid == c) else 0.0 for c in range(kc)])
+    want = cap["want_P_PR_PS"]
     with np.errstate(divide="ignore", invalid="ignore"):
         p_err = float(np.max(np.where(want != 0, np.abs(diag[:kc, :3] - want) / np.abs(want), np.abs(diag[:kc, :3]))))
-    melt = {}
-    for col, v in ((3, "SM"), (4, "IM")):
-        w = np.bincount(cid, weights=np.broadcast_to(getattr(m, "cell_vol_" + v), (n,)), minlength=kc)[:kc]
-        melt[f"vol_{v}_max_rel"] = float(np.max(np.abs(diag[:kc, col] - w)) / max(float(np.max(np.abs(w))), 1e-300))
-    mass = {"catchments": kc, "vol_P_PR_PS_max_rel": p_err, "vol_P_PR_PS_tolerance": 1e-6,
-            "P_max_exact": bool(np.array_equal(diag[:kc, 5], pmax)), **melt,
-            "note": "vol_SM / vol_IM reported, not gated: a melt-out flip moves a cell's melt by a step"}
+    mass = {"catchments": kc, "cells": plan["rows"] * nx, "vol_P_PR_PS_max_rel": p_err,
+            "vol_P_PR_PS_tolerance": 1e-6, "P_max_exact": bool(np.array_equal(diag[:kc, 5], cap["want_P_max"])),
+            "vs": "fp64 sums of the forcing frames the shard read (torch on the device), per catchment"}
     engine_desc = ("k_fused<float, READ_DEPTHS=false, CATCH=%s, QC=false, clean form>" % ("true" if args.catchments else "false")
                    if args.engine == "float32" else "k_fused<double, exact, READ_DEPTHS=false>")
     parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "rank": rank,
               "global_rows": [row0, row0 + rows - 1], "cells": n, "steps": pp["launch_steps"][1],
               "lead_in_steps": pp["launch_steps"][0], "steps_compared": steps, "launch_steps": pp["launch_steps"],
-              "timed_kernel_instance": engine_desc + f" in a {pp['launch_steps'][1]}-step launch, after a one-step "
-                                                     f"lead-in launch that reads the initial depths",
+              "timed_kernel_instance": engine_desc + f" in a {pp['launch_steps'][1]}-step launch over the whole "
+                                                     f"{plan['rows']}x{nx} shard (the bench handle's first, after a "
+                                                     f"one-step lead-in launch that reads the initial depths)",
               "nan_safe_launches": ns, "outputs": list(HIST), "max_floored_rel": err,
               "max_floored_rel_by_output": by_out, "tolerance": tol, "frac_above_pure_rel_1e-5": pure,
               "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"], "flip_ratio": rule["ratio"],
@@ -527,9 +556,10 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
         eng.get_field_device(name, blk[i], index=0)
     step_b, launch_b = bytes_model(4)
     out = {"cells": n, "steps": steps,
-           "protocol": "per step: tfg_set_inputs (device f32 [5][n]) + tfg_step(1); queued: the same inputs into "
-                       f"{steps} frames, then one {steps}-step launch"}
-    for mode in ("per_step", "queued"):
+           "protocol": "per step: tfg_set_inputs (device f32 [5][n]) + tfg_step(1)" + (
+               f"; queued: the same inputs into {steps} frames, then one {steps}-step launch" if args.dropin_queued
+               else "")}
+    for mode in ("per_step", "queued") if args.dropin_queued else ("per_step",):
         ns0 = eng.nan_safe_launches()
         ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -706,13 +736,20 @@ def main():
         lateral_conduction(eng, cfg.k_snow, cfg.k_ice, 30.0, 30.0, distributed=world > 1)
         cond_ms.append((time.perf_counter() - t) * 1e3)
 
+    # the parity check's GPU side: the handle's first launches (a one-step
+    # lead-in, then one whole launch of the timed depth over the whole shard)
+    cap = None
+    if not args.no_parity:
+        cap = capture_parity(eng, args, plan, world, torch, local)
     # warmup (untimed): the requested steps, and at least one whole launch of
-    # the timed depth.  The first full-depth launch after a short warm-up runs
-    # 10-29 ms long on 8192/N-row slabs (scripts/gpu_slab_warmup.sh,
-    # profiles/r2p_slab_warmup.json: 1024 x 8192 after --warmup 5: 43.3 ms, then
-    # 14.8 and 14.3 ms); after one such launch every later one is steady.
+    # the timed depth (the parity launch counts).  The first full-depth launch
+    # after a short warm-up runs 10-29 ms long on 8192/N-row slabs
+    # (scripts/gpu_slab_warmup.sh, profiles/r2p_slab_warmup.json: 1024 x 8192
+    # after --warmup 5: 43.3 ms, then 14.8 and 14.3 ms); after one such launch
+    # every later one is steady.
     warm_steps = warmup_steps(args.warmup, args.fuse)
-    eng.run(warm_steps)
+    eng.run(warm_steps - (eng.step_index - 1 if cap else 0))
+    warm_run = eng.step_index
     barrier()
     ns_before = eng.nan_safe_launches() if args.engine == "float32" else 0
     # Whole fused launches, and at least MIN_LAUNCHES of them, so that a short
@@ -745,8 +782,9 @@ def main():
     torch.cuda.empty_cache()
     # every rank checks its own shard's first rows against the oracle (outside the timed region)
     parity = numpy_leg = None
-    if not args.no_parity:
-        parity, numpy_leg = sample_parity(args, plan, world, rank, local, _cpu_threads())
+    if cap is not None:
+        parity, numpy_leg = sample_parity(args, plan, world, rank, _cpu_threads(), cap)
+        del cap
     own = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), **device_record(torch, local),
            "row0": row0, "rows": rows, "elapsed_s": elapsed, "launch_ms_mean": float(launch_ms.mean()),
            "launch_ms_min": float(launch_ms.min()), "launch_ms_max": float(launch_ms.max()),
@@ -799,7 +837,7 @@ def main():
                          "ms_mean": float(launch_ms.mean()), "ms_max": float(launch_ms.max()),
                          "ms_each": [round(float(x), 3) for x in launch_ms]},
             "warmup": args.warmup,
-            "warmup_steps_run": warm_steps,
+            "warmup_steps_run": warm_run,  # untimed steps before the timed region (incl. the parity launches)
             "ms_per_step": elapsed / steps * 1e3,
             "higher_is_better": True,
             "scaling": args.scaling,

@@ -235,9 +235,10 @@ int tfg_update_many(tfg_handle* const* hs, int m, const double* const* src, cons
  * history slot -- exact checkpoint / restart. */
 #define TFG_PREV_DEPTH (-1)
 
-/* Copy n cells of a field out.  `index` is the history slot for TFG_OUT_*
- * (except H_SWE/H_IWE, which are state; TFG_PREV_DEPTH above), the frame for
- * TFG_IN_*.
+/* Copy n cells of a field out: n = ny*nx, or fewer for the first n cells in
+ * row-major order (a leading block of rows, e.g. a sample of a large shard).
+ * `index` is the history slot for TFG_OUT_* (except H_SWE/H_IWE, which are
+ * state; TFG_PREV_DEPTH above), the frame for TFG_IN_*.
  * Replaces: get_value / get_value_ptr (:1810-1828). */
 int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n,
                   int dst_on_device);

@@ -69,9 +69,8 @@ def main():
             e.fill_synthetic(20251001, diurnal_table(24), nx_global=nx)
             e.run(k * max(2, 3840 // k))  # warm-up
             e.sync()
-            n_pad = -(-e.n // 64) * 64
-            n_pad += 512 if n_pad >= 1 << 20 else 0  # tfg_create's plane skew
-            nwg = min(131072, -(-n_pad // 256))  # fused_blocks: one workgroup per 256-cell chunk, capped
+            n_work = -(-e.n // 64) * 64  # the cells k_fused steps (the plane skew is not stepped)
+            nwg = min(131072, -(-n_work // 256))  # fused_blocks: one workgroup per 256-cell chunk, capped
             runs = []
             for _ in range(3):
                 e.run(k)

@@ -144,7 +144,7 @@ def test_weak_scaling_stays_behind_its_flag():
 def test_bench_prints_one_json_line_with_the_contract_keys():
     cmd = [sys.executable, str(ROOT / "bench.py"), "--ny", "256", "--nx", "1024", "--steps", "48", "--warmup", "24",
            "--fuse", "24", "--cpu-cells", "4096", "--cpu-steps", "48", "--parity-cells", "2048",
-           "--dropin-instances", "64"]
+           "--dropin-instances", "64", "--dropin-queued"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -167,9 +167,12 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     sp = d["sample_parity"]
     assert sp["genuine_mismatches"] == 0 and sp["max_floored_rel"] <= sp["tolerance"]
     assert sp["ok"] and sp["melt_out_flips"] <= sp["flip_budget"] and "flips_fp64_baseline" in sp
-    # the check runs the timed launch depth after a one-step lead-in, on the clean step form
+    # the check reads the bench handle's own first launches: a one-step lead-in, then a whole launch of the
+    # timed depth over the whole shard, on the clean step form; the untimed steps include them
     assert sp["steps"] == 24 and sp["launch_steps"] == [1, 24] and sp["steps_compared"] == 25
     assert sp["cells"] == 2048 and sp["nan_safe_launches"] == 0 and sp["mass_balance"]["P_max_exact"]
+    assert "256x1024 shard" in sp["timed_kernel_instance"] and sp["mass_balance"]["cells"] == 256 * 1024
+    assert sp["mass_balance"]["vol_P_PR_PS_max_rel"] <= 1e-6 and d["warmup_steps_run"] == 25
     assert d["ranks"]["ranks"][0]["sample_parity"]["ok"]
     # the drop-in legs: per-step K = 1 launches from device inputs, and queued steps; defer_update instances
     g = d["dropin_per_step_grid"]

@@ -1321,7 +1321,7 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
 int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
-  if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
+  if (n <= 0 || n > h->n) return fail(h, TFG_ERR_ARG, "n outside 1..ny*nx");  // n < ny*nx: the first n cells
   HIPCHK(h, hipSetDevice(h->device));
   if ((field == TFG_OUT_H_SNOW || field == TFG_OUT_H_ICE) && index == TFG_PREV_DEPTH) {
     // the fp64 previous-step depth the next step reads (checkpoint / restart)
@@ -1402,7 +1402,7 @@ int check_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
 // The launches of nsteps steps whose uniforms the device reads at d_u (u is
 // the host copy of the same records).
 int fused_blocks(const tfg_handle* h) {
-  const int64_t ngroups = h->n_pad / kCellsPerThread;
+  const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;  // k_fused's cells: the skew is not stepped
   return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
 }
 

@@ -252,7 +252,10 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
 #endif
 
   const int64_t n_pad = a.n_pad;
-  const int64_t ngroups = n_pad / C;
+  // the cells rounded up to a wave, not the plane stride: the plane skew
+  // (tfg_create) is address padding, and stepping it cost a partial extra
+  // round of workgroups at 1024^2 (4098 chunks for 4096 resident slots)
+  const int64_t ngroups = ((a.n + 63) & ~(int64_t)63) / C;
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).

@@ -111,18 +111,20 @@ class GlacierEngine:
             code = nat.F32 if a.dtype == np.float32 else nat.F64
         self._chk(self.lib.tfg_set_field(self.h, fid, index, a.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
 
-    def get_field(self, name: str, index: int | None = None, dtype=np.float64) -> np.ndarray:
-        """Host copy of a field.  Outputs default to the newest history slot."""
+    def get_field(self, name: str, index: int | None = None, dtype=np.float64, cells: int | None = None) -> np.ndarray:
+        """Host copy of a field (its first `cells` cells: a leading block of
+        rows; default all).  Outputs default to the newest history slot."""
         fid = nat.FIELD[name]
+        n = self.n if cells is None else int(cells)
         if index is None:
             index = self.last_hist if name in ("h_snow", "SM", "h_ice", "IM", "M_total", "RH") else 0
         if name == "catch_id":
-            out = np.empty(self.n, dtype=np.int32)
+            out = np.empty(n, dtype=np.int32)
             code = nat.I32
         else:
-            out = np.empty(self.n, dtype=dtype)
+            out = np.empty(n, dtype=dtype)
             code = nat.F32 if out.dtype == np.float32 else nat.F64
-        self._chk(self.lib.tfg_get_field(self.h, fid, index, out.ctypes.data_as(ctypes.c_void_p), code, self.n, 0))
+        self._chk(self.lib.tfg_get_field(self.h, fid, index, out.ctypes.data_as(ctypes.c_void_p), code, n, 0))
         return out
 
     def get_field_device(self, name: str, out, index: int | None = None):
