@@ -216,6 +216,15 @@ def parse():
     return ap.parse_args()
 
 
+_T0 = time.perf_counter()
+
+
+def note(msg: str) -> None:
+    """A progress line on stderr (stdout carries only the JSON line): a long
+    phase (the oracle of a deep parity launch, the CPU baseline) stays visible."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def _cpu_threads() -> int:
     """Host threads for the C baseline: the process's CPU share (16 on a one-GPU
     box, where OMP_NUM_THREADS is set to it), never the whole machine."""
@@ -374,10 +383,13 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
         r = m.step(*(forcing[v][frames[k]] for v in FORCING), jd[k], tsn[k])
         for v in HIST:
             ref[v][k] = r[v]
+        if k % 64 == 63:
+            note(f"parity: numpy oracle step {k + 1}/{steps} on {n} cells")
     t_np = time.perf_counter() - t0
     numpy_leg = {"value": n * steps / t_np, "unit": "cell-updates/s", "cores": 1, "kind": "port",
                  "sample": f"oracle/tfg_oracle.py (numpy fp64, single thread) on {n} cells x {steps} steps "
                            f"({t_np:.1f} s), the reference of the parity check"}
+    note("parity: C oracle (fp64 baseline of the flip rule)")
     c64, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=frames, hist=True, nthreads=threads)
     tol = 1e-5 if args.engine == "float32" else 1e-10
     flip64, genuine64 = melt_out_flips({v: c64[v] for v in HIST}, ref, tol)
@@ -741,6 +753,7 @@ def main():
     cap = None
     if not args.no_parity:
         cap = capture_parity(eng, args, plan, world, torch, local)
+        note(f"parity launches done ({eng.step_index} steps)")
     # warmup (untimed): the requested steps, and at least one whole launch of
     # the timed depth (the parity launch counts).  The first full-depth launch
     # after a short warm-up runs 10-29 ms long on 8192/N-row slabs
@@ -768,6 +781,7 @@ def main():
         ev[i][1].record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
+    note(f"timed region: {n_launch} launches of {args.fuse} steps in {elapsed:.3f} s")
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
     cells = rows * args.nx
     diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
@@ -805,9 +819,11 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            note("CPU baseline (C oracle)")
             cpu = cpu_baseline(args)
         dropin_many = None
         if world == 1 and not args.no_dropin and args.dropin_instances > 0:
+            note("drop-in leg: defer_update instances")
             dropin_many = dropin_instances_leg(args, local)
         if world > 1:
             parity = parity_summary([r["sample_parity"] for r in ranks["ranks"]]) if not args.no_parity else None

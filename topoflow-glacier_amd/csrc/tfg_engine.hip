@@ -1402,7 +1402,11 @@ int check_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
 // The launches of nsteps steps whose uniforms the device reads at d_u (u is
 // the host copy of the same records).
 int fused_blocks(const tfg_handle* h) {
+#if TFG_STEP_SKEW
+  const int64_t ngroups = h->n_pad / kCellsPerThread;
+#else
   const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;  // k_fused's cells: the skew is not stepped
+#endif
   return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
 }
 

@@ -206,6 +206,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #ifndef TFG_WG_PERM
 #define TFG_WG_PERM 0
 #endif
+#ifndef TFG_STEP_SKEW
+#define TFG_STEP_SKEW 0
+#endif
 #ifdef TFG_WG_TIMING  // diagnostic builds (tests/diagnostics/wg_timeline.py): for the first
                       // TFG_WG_TIMING workgroups of every k_fused launch, the wall clock
                       // (100 MHz) at start and end and the XCC / CU it ran on
@@ -255,7 +258,11 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
   // the cells rounded up to a wave, not the plane stride: the plane skew
   // (tfg_create) is address padding, and stepping it cost a partial extra
   // round of workgroups at 1024^2 (4098 chunks for 4096 resident slots)
+#if TFG_STEP_SKEW  // measurement switch: step the whole plane stride, skew included (round 3)
+  const int64_t ngroups = n_pad / C;
+#else
   const int64_t ngroups = ((a.n + 63) & ~(int64_t)63) / C;
+#endif
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
