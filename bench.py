@@ -79,6 +79,7 @@ def launch_bytes_per_cell(fuse: int, elem: int = 4, catchments: bool = False, qc
     step, launch = bytes_model(elem, catchments, qc)
     return step * fuse + launch
 
+PARITY_CELL_STEPS = 262144 * 129
 MIN_LAUNCHES = 6
 # Why 6: the first launch after the barrier that opens the timed region runs
 # 0.5-3.6 ms long at every shape and warm-up length (profiles/r3c_slab_skew_study.jsonl,
@@ -285,9 +286,11 @@ def parity_plan(args, plan: dict, world: int) -> dict:
     timed depth over the whole shard (capture_parity): the timed kernel
     instance at the timed launch length and shape (at K = 128 the
     three-register-set step loop ends in its two-step tail)."""
-    want = args.parity_cells or (262144 if world == 1 else 65536)
-    rows = max(1, min(plan["rows"], want // args.nx))
     k = args.parity_steps or args.fuse
+    # the oracle's work bounded to that of 262144 cells x 129 steps (the N = 1
+    # headline check, ~60 s of host time): deeper launches check fewer rows
+    want = args.parity_cells or min(262144 if world == 1 else 65536, PARITY_CELL_STEPS // (1 + k))
+    rows = max(1, min(plan["rows"], want // args.nx))
     return {"row0": plan["row0"], "rows": rows, "cells": rows * args.nx, "launch_steps": [1, k], "steps": 1 + k}
 
 
@@ -392,7 +395,10 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
     note("parity: C oracle (fp64 baseline of the flip rule)")
     c64, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=frames, hist=True, nthreads=threads)
     tol = 1e-5 if args.engine == "float32" else 1e-10
+    note("parity: melt-out flips of the fp64 baseline")
     flip64, genuine64 = melt_out_flips({v: c64[v] for v in HIST}, ref, tol)
+    del c64
+    note("parity: melt-out flips of the GPU")
     flip, genuine = melt_out_flips(gpu, ref, tol)
     ok = valid_mask(flip, steps)
     by_out = {v: _floored_rel(gpu[v][ok], ref[v][ok])[0] for v in HIST}

@@ -1405,7 +1405,7 @@ int fused_blocks(const tfg_handle* h) {
 #if TFG_STEP_SKEW
   const int64_t ngroups = h->n_pad / kCellsPerThread;
 #else
-  const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;  // k_fused's cells: the skew is not stepped
+  const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;  // k_fused's cells only
 #endif
   return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
 }

@@ -207,7 +207,9 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
 #define TFG_WG_PERM 0
 #endif
 #ifndef TFG_STEP_SKEW
-#define TFG_STEP_SKEW 0
+#define TFG_STEP_SKEW 1  // k_fused steps the plane stride, skew cells included (0: only the cells;
+                         // same-box A/B neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, 0 at 4096^2,
+                         // profiles/r4d_ab_skew.json)
 #endif
 #ifdef TFG_WG_TIMING  // diagnostic builds (tests/diagnostics/wg_timeline.py): for the first
                       // TFG_WG_TIMING workgroups of every k_fused launch, the wall clock
@@ -255,12 +257,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
 #endif
 
   const int64_t n_pad = a.n_pad;
-  // the cells rounded up to a wave, not the plane stride: the plane skew
-  // (tfg_create) is address padding, and stepping it cost a partial extra
-  // round of workgroups at 1024^2 (4098 chunks for 4096 resident slots)
-#if TFG_STEP_SKEW  // measurement switch: step the whole plane stride, skew included (round 3)
+#if TFG_STEP_SKEW  // the whole plane stride, the skew's padding cells included
   const int64_t ngroups = n_pad / C;
-#else
+#else             // the cells rounded up to a wave
   const int64_t ngroups = ((a.n + 63) & ~(int64_t)63) / C;
 #endif
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
