@@ -410,6 +410,12 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
             rel = np.where(rv != 0, np.abs(gv - rv) / np.abs(rv), np.where(gv != rv, np.inf, 0.0))
         pure[v] = float(np.mean(rel > 1e-5))
     rule = flip_rule(int((flip >= 0).sum()), int((flip64 >= 0).sum()))
+    examples = []  # the first genuine mismatches, with the state around them (diagnosis)
+    for c, k, vs in genuine[:6]:
+        j = [max(k - 2, 0), max(k - 1, 0), k]
+        examples.append({"cell": int(c), "global_row": int(row0 + c // nx), "step": int(k), "outputs": vs,
+                         **{f"{v}_gpu_ref_steps_k-2_k-1_k": [[float(gpu[v][i, c]), float(ref[v][i, c])] for i in j]
+                            for v in ("h_snow", "SM", "h_ice", "IM")}})
     # the shard's mass-balance integrals after the same steps (:558-624), per catchment
     kc = max(args.catchments, 1)
     want = cap["want_P_PR_PS"]
@@ -430,7 +436,7 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
               "max_floored_rel_by_output": by_out, "tolerance": tol, "frac_above_pure_rel_1e-5": pure,
               "melt_out_flips": rule["flips"], "flips_fp64_baseline": rule["fp64_flips"], "flip_ratio": rule["ratio"],
               "flip_budget": rule["budget"], "flip_rule": rule["rule"], "genuine_mismatches": len(genuine),
-              "fp64_baseline_genuine_mismatches": len(genuine64), "mass_balance": mass,
+              "fp64_baseline_genuine_mismatches": len(genuine64), "genuine_examples": examples, "mass_balance": mass,
               "ok": bool(err <= tol and not genuine and rule["ok"] and ns == 0 and p_err <= 1e-6
                          and mass["P_max_exact"])}
     return parity, numpy_leg

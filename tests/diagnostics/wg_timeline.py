@@ -80,6 +80,12 @@ def main():
                 rec = np.zeros((131072, 3), np.uint64)
                 nat.check(L.tfg_debug_wg_times(rec.ctypes.data, 131072))
                 runs.append(timeline(rec[:nwg]))
+                if nwg <= 20000 and os.environ.get("TFG_WG_RAW"):  # per-workgroup records: start, end (us), XCC, CU
+                    r = rec[:nwg]
+                    t0 = int(r[:, 0].min())
+                    runs[-1]["raw_start_end_xcc_cu"] = [
+                        [round((int(a) - t0) * TICK_NS / 1e3, 2), round((int(b) - t0) * TICK_NS / 1e3, 2), int(c >> 32),
+                         int(c & 0xFFFFFFFF)] for a, b, c in r]
                 print(f"{ny}x{nx} K={k}", json.dumps({kk: v for kk, v in runs[-1].items() if kk != "xcc_mean_dur_us"}),
                       flush=True)
             res[f"{ny}x{nx}_K{k}"] = runs
