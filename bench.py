@@ -767,13 +767,16 @@ def main():
         cap = capture_parity(eng, args, plan, world, torch, local)
         note(f"parity launches done ({eng.step_index} steps)")
     # warmup (untimed): the requested steps, and at least one whole launch of
-    # the timed depth (the parity launch counts).  The first full-depth launch
-    # after a short warm-up runs 10-29 ms long on 8192/N-row slabs
-    # (scripts/gpu_slab_warmup.sh, profiles/r2p_slab_warmup.json: 1024 x 8192
-    # after --warmup 5: 43.3 ms, then 14.8 and 14.3 ms); after one such launch
-    # every later one is steady.
+    # the timed depth.  The first full-depth launch after a short warm-up runs
+    # 10-29 ms long on 8192/N-row slabs (scripts/gpu_slab_warmup.sh,
+    # profiles/r2p_slab_warmup.json: 1024 x 8192 after --warmup 5: 43.3 ms, then
+    # 14.8 and 14.3 ms); after one such launch every later one is steady.  The
+    # parity launches count, but the host reads that follow them leave the GPU
+    # idle (the first timed launch then ran 5-11 ms long at 8192^2,
+    # profiles/r4e_bench_driver_traced.json), so one more whole launch runs
+    # right before the timed region.
     warm_steps = warmup_steps(args.warmup, args.fuse)
-    eng.run(warm_steps - (eng.step_index - 1 if cap else 0))
+    eng.run(max(warm_steps - (eng.step_index - 1), args.fuse) if cap else warm_steps)
     warm_run = eng.step_index
     barrier()
     ns_before = eng.nan_safe_launches() if args.engine == "float32" else 0

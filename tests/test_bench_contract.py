@@ -172,7 +172,7 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert sp["steps"] == 24 and sp["launch_steps"] == [1, 24] and sp["steps_compared"] == 25
     assert sp["cells"] == 2048 and sp["nan_safe_launches"] == 0 and sp["mass_balance"]["P_max_exact"]
     assert "256x1024 shard" in sp["timed_kernel_instance"] and sp["mass_balance"]["cells"] == 256 * 1024
-    assert sp["mass_balance"]["vol_P_PR_PS_max_rel"] <= 1e-6 and d["warmup_steps_run"] == 25
+    assert sp["mass_balance"]["vol_P_PR_PS_max_rel"] <= 1e-6 and d["warmup_steps_run"] == 49  # lead-in + parity launch + one more whole launch
     assert d["ranks"]["ranks"][0]["sample_parity"]["ok"]
     # the drop-in legs: per-step K = 1 launches from device inputs, and queued steps; defer_update instances
     g = d["dropin_per_step_grid"]
