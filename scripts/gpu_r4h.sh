@@ -12,7 +12,7 @@ run() { name=$1; shift
   rc=$?; echo "$name rc=$rc"; stop $rc; [ $rc -eq 0 ] || { tail -5 gpurun_out/${tag}_$name.err; return $rc; }
   python3 -c "
 import json; d = json.loads([l for l in open('gpurun_out/${tag}_$name.json') if l.startswith('{')][-1]); sp = d['sample_parity']
-print('$name', '%.2f G' % (d['value'] / 1e9), 'K', d['config']['fuse_steps'], 'ok', sp['ok'], 'cells', sp['cells'], 'err %.2e' % sp['max_floored_rel'], 'flips', sp['melt_out_flips'], '/', sp['flips_fp64_baseline'], 'genuine', sp['genuine_mismatches'], 'onsets', sp.get('melt_onsets_explained'), 'depletion', sp.get('depletion_steps_explained'), 'first launches', d['launches']['ms_each'][:3], flush=True)"; }
+print('$name', '%.2f G' % (d['value'] / 1e9), 'K', d['config']['fuse_steps'], 'ok', sp['ok'], 'cells', sp['cells'], 'err %.2e' % sp['max_floored_rel'], 'flips', sp['melt_out_flips'], '/', sp['flips_fp64_baseline'], 'genuine', sp['genuine_mismatches'], 'onsets', sp.get('melt_onsets_explained'), 'depletion', sp.get('depletion_steps'), 'first launches', d['launches']['ms_each'][:3], flush=True)"; }
 run cfg2_auto --ny 1024 --nx 1024 --steps 2304 --no-cpu-baseline --no-dropin &&
 run shard_n8 --ny 1024 --nx 8192 --steps 2304 --no-cpu-baseline --no-dropin &&
 run shard_n4 --ny 2048 --nx 8192 --steps 2304 --no-cpu-baseline --no-dropin &&
