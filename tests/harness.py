@@ -113,9 +113,8 @@ def depletion_steps(gpu: dict, ref: dict, cfg: dict, rtol: float = 1e-5) -> np.n
     exactly zero at the step in both trajectories, only SM / IM / M_total
     differ, and the difference of the melted amount (rate x dt x 3600 x w,
     w = rho_H2O / rho_snow or / rho_ice, in m of depth) is within the depth's
-    tolerance at the step before.  Such steps are marked whether or not the
-    rate is also within its own tolerance (the rate is then held to the depth's
-    tolerance at every such step); later steps are compared as usual."""
+    tolerance at the step before.  Only entries outside the rate's own
+    tolerance are marked; later steps are compared as usual."""
     c = dict(O.CFG_DEFAULTS)
     c.update(cfg)
     sec = float(c["dt"]) * 3600.0
@@ -137,9 +136,12 @@ def depletion_steps(gpu: dict, ref: dict, cfg: dict, rtol: float = 1e-5) -> np.n
     tol_mt = (np.where(dry["snow"], tol_depth["snow"] / w["snow"], 0.0)
               + np.where(dry["ice"], tol_depth["ice"] / w["ice"], 0.0))
     ok_mt = (dry["snow"] | dry["ice"]) & (np.abs(G["M_total"] - R["M_total"]) * sec <= tol_mt)
+    any_bad = np.zeros((nsteps, ncell), dtype=bool)
+    for v in bad.values():
+        any_bad |= v
     rh_ok = ~bad["RH"] if "RH" in bad else np.ones((nsteps, ncell), dtype=bool)
-    # every such step, in or out of the rate's own tolerance: its rates are held to the depth's
-    return ((dry["snow"] | dry["ice"]) & ~bad["h_snow"] & ~bad["h_ice"] & rh_ok & (~bad["SM"] | ok_amount["snow"])
+    # only the entries outside the rate's own tolerance need (and get) the explanation
+    return (any_bad & ~bad["h_snow"] & ~bad["h_ice"] & rh_ok & (~bad["SM"] | ok_amount["snow"])
             & (~bad["IM"] | ok_amount["ice"]) & (~bad["M_total"] | ok_mt))
 
 

@@ -183,6 +183,24 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert rf["traffic"] is None and ts["reason"]
 
 
+@pytest.mark.gpu
+def test_bench_parity_holds_at_the_deep_launches_of_the_multi_gpu_lines():
+    """The N = 4 / N = 8 lines fuse 384 steps; the synthetic snowpacks start
+    to run dry after ~300 steps, so their parity checks meet depletion steps and
+    melt onsets, which the GPU suite's rules explain (tests/harness.py
+    depletion_steps, melt_onsets).  One 384-step launch over 64 x 1024 cells,
+    checked the way each rank of those lines checks its own rows."""
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--ny", "64", "--nx", "1024", "--fuse", "384", "--steps", "768",
+           "--warmup", "0", "--no-cpu-baseline", "--no-dropin"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    sp = d["sample_parity"]
+    assert sp["steps"] == 384 and sp["cells"] == 65536 and sp["genuine_mismatches"] == 0, sp.get("genuine_examples")
+    assert sp["depletion_steps"] > 0 and sp["melt_onsets_explained"] <= sp["melt_onset_budget"]
+    assert sp["max_floored_rel"] <= sp["tolerance"] and sp["ok"], sp["max_floored_rel_at"]
+
+
 def test_rank_report_names_the_devices_and_the_slowest_rank():
     """The per-rank record a multi-GPU line carries (bench.rank_report): ranks
     in order, the slowest one, max/min span, distinct GPUs; two RCCL ranks on
