@@ -735,6 +735,33 @@ def test_batched_io_equals_per_field_io(engine):
 
 
 @pytest.mark.parametrize("engine", ["float32", "float64"])
+def test_leading_prefix_reads_equal_whole_field_reads(engine):
+    """tfg_get_field with n < ny*nx reads the first n cells (bench.py's parity
+    sample of a large shard): history slots, state, frames, the snowfall
+    window and the fp64 previous-step depths, against the whole-field read;
+    n outside 1..ny*nx is refused."""
+    from topoflow_glacier import _native as nat
+
+    ny, nx = 7, 37
+    e = make_engine(BASE_CFG, ny, nx, engine, n_frames=24, hist_depth=4, fuse_steps=4)
+    try:
+        e.fill_synthetic(5, synthetic_inputs(5, ny, nx, 24)[1])
+        e.run(6)
+        e.sync()
+        for m in (1, nx, 3 * nx + 5, ny * nx):
+            for name, idx in (("SM", 1), ("h_snow", 2), ("h_swe", 0), ("T_air", 5), ("window", 3),
+                              ("h_ice", nat.PREV_DEPTH)):
+                for dt in (np.float32, np.float64):
+                    whole = e.get_field(name, index=idx, dtype=dt)
+                    np.testing.assert_array_equal(e.get_field(name, index=idx, dtype=dt, cells=m), whole[:m])
+        for bad in (0, ny * nx + 1):
+            with pytest.raises(nat.NativeError):
+                e.get_field("SM", index=0, cells=bad)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("engine", ["float32", "float64"])
 @pytest.mark.parametrize("frames,hist", [(1, 1), (3, 2)])
 def test_update_io_equals_set_step_get(engine, frames, hist):
     """tfg_update (one synchronous call through the pinned, device-mapped
