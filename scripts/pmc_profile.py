@@ -55,14 +55,14 @@ def calibration(d: Path, cells: int, steps: int):
     """Counter KiB x 1024 / known bytes for each calibration kernel (first
     dispatch is the warm-up; all dispatches move the same bytes)."""
     kernels = {  # tools/hbm_mix.hip k_mix<R, W, V, NT>
-        "read only 4 B/lane": ("k_mix<7, 0, 1, false>", "FETCH_SIZE", 7),
-        "read only 16 B/lane": ("k_mix<7, 0, 4, false>", "FETCH_SIZE", 7),
-        "read only 8 B/lane": ("k_mix<7, 0, 2, false>", "FETCH_SIZE", 7),
-        "write only 8 B/lane nt": ("k_mix<0, 7, 2, true>", "WRITE_SIZE", 7),
-        "write only 4 B/lane": ("k_mix<0, 7, 1, false>", "WRITE_SIZE", 7),
-        "write only 4 B/lane nt": ("k_mix<0, 7, 1, true>", "WRITE_SIZE", 7),
-        "k_fused mix reads 4 B/lane nt": ("k_mix<6, 7, 1, true>", "FETCH_SIZE", 6),
-        "k_fused mix writes 4 B/lane nt": ("k_mix<6, 7, 1, true>", "WRITE_SIZE", 7),
+        "read only 4 B/lane": ("k_mix<7, 0, 1, false,", "FETCH_SIZE", 7),
+        "read only 16 B/lane": ("k_mix<7, 0, 4, false,", "FETCH_SIZE", 7),
+        "read only 8 B/lane": ("k_mix<7, 0, 2, false,", "FETCH_SIZE", 7),
+        "write only 8 B/lane nt": ("k_mix<0, 7, 2, true,", "WRITE_SIZE", 7),
+        "write only 4 B/lane": ("k_mix<0, 7, 1, false,", "WRITE_SIZE", 7),
+        "write only 4 B/lane nt": ("k_mix<0, 7, 1, true,", "WRITE_SIZE", 7),
+        "k_fused mix reads 4 B/lane nt": ("k_mix<6, 7, 1, true,", "FETCH_SIZE", 6),
+        "k_fused mix writes 4 B/lane nt": ("k_mix<6, 7, 1, true,", "WRITE_SIZE", 7),
     }
     out = {}
     for name, (kern, counter, planes) in kernels.items():

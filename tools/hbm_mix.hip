@@ -64,6 +64,9 @@ __global__ __launch_bounds__(256) void k_mix(const float* __restrict__ in, float
         splat(o, acc + (float)w);
         T* dst = reinterpret_cast<T*>(fo + (size_t)w * ps) + i;
         if constexpr (POL > 0) { static_assert(V == 1, "policy stores are 4 B"); store_pol<POL>((float*)dst, hsum(o)); }
+        else if constexpr (NT && V == 2)  // 8-byte lanes: the nontemporal builtin takes no float2
+          __builtin_nontemporal_store(*reinterpret_cast<const unsigned long long*>(&o),
+                                      reinterpret_cast<unsigned long long*>(dst));
         else if constexpr (NT) __builtin_nontemporal_store(o, dst);
         else *dst = o;
       }
