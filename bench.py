@@ -211,9 +211,6 @@ def parse():
     ap.add_argument("--dt", type=float, default=1.0, help="time step [h] (BASELINE config 5: 0.25)")
     ap.add_argument("--catchments", type=int, default=0,
                     help="K > 0: per-catchment mass balance over a K-catchment block raster (BASELINE config 5)")
-    ap.add_argument("--one-call", action="store_true",
-                    help="time the steps as ONE engine call (tfg_step of all timed steps) instead of one call per "
-                         "launch; with TFG_WQ=1 the engine then runs them as one work-queue launch (measurement)")
     ap.add_argument("--conduction", action="store_true",
                     help="the optional lateral heat-conduction term: Qc re-evaluated (with the one-row halo swap "
                          "between ranks) before every fused launch, inside the timed region")
@@ -831,25 +828,16 @@ def main():
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
     barrier()
     t0 = time.perf_counter()
-    if args.one_call and not args.conduction:
-        # one engine call for all timed steps: the launches it makes are timed as one span
-        ev[0][0].record(stream)
-        eng.run(steps)
-        ev[0][1].record(stream)
-        ev = ev[:1]
-    else:
-        for i in range(n_launch):
-            if args.conduction:
-                conduct()
-            ev[i][0].record(stream)
-            eng.run(args.fuse)
-            ev[i][1].record(stream)
+    for i in range(n_launch):
+        if args.conduction:
+            conduct()
+        ev[i][0].record(stream)
+        eng.run(args.fuse)
+        ev[i][1].record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
     note(f"timed region: {n_launch} launches of {args.fuse} steps in {elapsed:.3f} s")
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    if len(ev) == 1 and n_launch > 1:  # --one-call: the span per launch's worth of steps
-        launch_ms = np.full(n_launch, launch_ms[0] / n_launch)
     cells = rows * args.nx
     diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
     bytes_launch = cells * launch_bytes_per_cell(args.fuse, elem, args.catchments > 0, args.conduction)

@@ -1063,43 +1063,3 @@ def test_device_sets_stay_stream_ordered_and_are_checked_lazily():
     assert (da, db, dc) == (1, 1, 2)  # device sets: the short launch NaN-safe, the long one checked clean
     np.testing.assert_array_equal(ho1, do1)
     np.testing.assert_array_equal(ho2, do2)
-
-
-@pytest.mark.parametrize("ny,nx,fuse,nsteps", [(64, 1024, 24, 24 * 5 + 7), (8, 100, 16, 16 * 3), (1, 64, 8, 40)])
-def test_work_queue_launch_equals_one_launch_per_range(monkeypatch, ny, nx, fuse, nsteps):
-    """TFG_WQ=1 (measurement mode): the steps of one engine call run as ONE
-    work-queue launch whose resident workgroups pull (chunk, range) items from
-    per-XCD queues, a range of a chunk waiting for its previous range
-    (k_fused<..., WQ>, tfg_fused.hpp wq_next / wq_done).  The arithmetic per
-    cell is the launch-per-range kernel's, so every output slot, the state and
-    the snowfall window must be identical bit for bit; only the mass-balance
-    sums may differ in their last bits (the cells fold in another order)."""
-    from topoflow_glacier import _native as nat
-
-    outs = []
-    for wq in ("0", "1"):
-        monkeypatch.setenv("TFG_WQ", wq)
-        e = make_engine(BASE_CFG, ny, nx, "float32", n_frames=24, hist_depth=fuse, fuse_steps=fuse)
-        try:
-            e.fill_synthetic(11, synthetic_inputs(11, ny, nx, 24)[1])
-            e.run(1)  # the lead-in launch reads the initial depths (never a work-queue launch)
-            e.run(nsteps)
-            e.sync()
-            got = {f"{v}_{k}": e.get_field(v, index=k, dtype=np.float32) for v in OUT_NAMES if v not in ("h_swe", "h_iwe")
-                   for k in range(fuse)}
-            for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n"):
-                got[v] = e.get_field(v)
-            for v in ("h_snow", "h_ice"):
-                got[v + "_prev"] = e.get_field(v, index=nat.PREV_DEPTH)
-            got["window"] = np.stack([e.get_field("window", index=j) for j in range(72)])
-            got["diag"] = e.diagnostics()
-            assert e.nan_safe_launches() == 0
-        finally:
-            e.close()
-        outs.append(got)
-    a, b = outs
-    for k in a:
-        if k == "diag":
-            np.testing.assert_allclose(b[k], a[k], rtol=1e-13)
-        else:
-            np.testing.assert_array_equal(b[k], a[k], err_msg=k)

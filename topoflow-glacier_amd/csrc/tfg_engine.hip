@@ -666,17 +666,6 @@ struct tfg_handle {
   int state_recheck = 0;             // launches before a dirty state is checked again
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
   bool force_ns = false;             // TFG_NANSAFE=1: every launch NaN-safe (tests)
-  // TFG_WQ=1 (measurement mode): the fp32 clean-form steps of one tfg_step call
-  // run as ONE work-queue launch of resident workgroups (k_fused<..., WQ>): a
-  // chunk's next range starts as soon as its previous one is done, so the drain
-  // at the end of every launch happens once per call instead of once per launch.
-  int wq = 0;                        // 1 on (XCDs probed), 0 off, -1 requested but unusable
-  int wq_nxcc = 0, wq_blocks = 0;
-  int* wq_buf = nullptr;             // [16] per-XCD counters, [16] error flag + pad, [nchunks] ranges done
-  int64_t wq_cap = 0;
-  int* wq_err_h = nullptr;           // pinned copy of the error flag of the last work-queue launch
-  hipEvent_t wq_ev = nullptr;
-  int64_t wq_launches = 0;
   std::string err;
 };
 
@@ -1085,7 +1074,6 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   h->max_blocks = (int)std::min<int64_t>(h->max_blocks, (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);
   if (const char* e = std::getenv("TFG_FUSE")) h->fuse = std::max(1, atoi(e));
   if (const char* e = std::getenv("TFG_NANSAFE")) h->force_ns = atoi(e) != 0;
-  if (const char* e = std::getenv("TFG_WQ")) h->wq = (atoi(e) != 0 && engine == TFG_F32) ? 2 : 0;  // 2: probe first
   if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "stream create failed"; return bail(TFG_ERR_HIP); }
   h->stream = h->own_stream;
   const int64_t np = h->n_pad;
@@ -1158,9 +1146,6 @@ int tfg_destroy(tfg_handle* h) {
   }
   if (h->out_d) (void)hipFree(h->out_d);
   if (h->out_h) (void)hipHostFree(h->out_h);
-  if (h->wq_buf) (void)hipFree(h->wq_buf);
-  if (h->wq_err_h) (void)hipHostFree(h->wq_err_h);
-  if (h->wq_ev) (void)hipEventDestroy(h->wq_ev);
   if (h->io_h) (void)hipHostFree(h->io_h);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
@@ -1529,97 +1514,6 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
   return TFG_OK;
 }
 
-__global__ void k_xcc_probe(int* __restrict__ out) {
-  if (threadIdx.x == 0) out[blockIdx.x] = (int)xcc_id();
-}
-
-// Work-queue mode set-up (TFG_WQ=1), once per handle: the XCD ids workgroups
-// report must be 0 .. n-1, every one seen (chunk c is served by XCD c % n), and
-// the resident workgroup count of the work-queue kernel.  Anything else: off.
-int wq_setup(tfg_handle* h, size_t lds) {
-  h->wq = -1;
-  hipDeviceProp_t prop;
-  HIPCHK(h, hipGetDeviceProperties(&prop, h->device));
-  int per_cu = 0;
-  HIPCHK(h, hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &per_cu, reinterpret_cast<const void*>(&k_fused<float, false, false, false, false, kCellsPerThread, false, true>),
-                kBlock, lds));
-  const int nprobe = prop.multiProcessorCount * 8;
-  int* d = nullptr;
-  HIPCHK(h, hipMalloc((void**)&d, (size_t)nprobe * 4));
-  hipLaunchKernelGGL(k_xcc_probe, nprobe, 64, 0, h->stream, d);
-  std::vector<int> ids(nprobe);
-  const hipError_t e1 = hipGetLastError();
-  const hipError_t e2 = hipMemcpyAsync(ids.data(), d, (size_t)nprobe * 4, hipMemcpyDeviceToHost, h->stream);
-  const hipError_t e3 = hipStreamSynchronize(h->stream);
-  (void)hipFree(d);
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(h, TFG_ERR_HIP, "work-queue XCD probe failed");
-  const int nx = *std::max_element(ids.begin(), ids.end()) + 1;
-  std::vector<int> seen(nx, 0);
-  for (int x : ids) seen[x] = 1;
-  if (per_cu < 1 || nx < 1 || nx > 16 || std::count(seen.begin(), seen.end(), 1) != nx) return TFG_OK;  // stays off
-  h->wq_nxcc = nx;
-  h->wq_blocks = std::min(per_cu * prop.multiProcessorCount, h->max_blocks);
-  HIPCHK(h, hipHostMalloc((void**)&h->wq_err_h, 4, hipHostMallocDefault));
-  *h->wq_err_h = 0;
-  HIPCHK(h, hipEventCreateWithFlags(&h->wq_ev, hipEventDisableTiming));
-  h->wq = 1;
-  return TFG_OK;
-}
-
-// The error flag of the last work-queue launch (a wait that gave up): read once
-// that launch has finished.
-int wq_check(tfg_handle* h) {
-  if (h->wq != 1 || !h->wq_launches) return TFG_OK;
-  HIPCHK(h, hipEventSynchronize(h->wq_ev));
-  if (*h->wq_err_h) return fail(h, TFG_ERR_HIP, "work-queue launch: a chunk waited too long for its previous range");
-  return TFG_OK;
-}
-
-// nsteps clean-form fp32 steps as one work-queue launch: ceil(nsteps / fuse)
-// ranges of `fuse` steps (the same bytes per range as a launch of `fuse`).
-int launch_wq(tfg_handle* h, const tfg_uniforms* d_u, int64_t nsteps, int fuse, size_t lds) {
-  if (int rc = wq_check(h)) return rc;
-#if TFG_STEP_SKEW
-  const int64_t ngroups = h->n_pad / kCellsPerThread;
-#else
-  const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;
-#endif
-  const int64_t nchunks = (ngroups + kBlock - 1) / kBlock;
-  if (h->wq_cap < 32 + nchunks) {
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (h->wq_buf) HIPCHK(h, hipFree(h->wq_buf));
-    h->wq_buf = nullptr;
-    HIPCHK(h, hipMalloc((void**)&h->wq_buf, (size_t)(32 + nchunks) * 4));
-    h->wq_cap = 32 + nchunks;
-  }
-  HIPCHK(h, hipMemsetAsync(h->wq_buf, 0, (size_t)(32 + nchunks) * 4, h->stream));
-  KArgs a;
-  a.p = h->dp;
-  a.K = fuse;
-  a.io_in = nullptr;
-  a.io_out = nullptr;
-  a.io_flag = nullptr;
-  a.io_seq = 0;
-  a.n_catch = h->n_catch;
-  a.n = h->n;
-  a.n_pad = h->n_pad;
-  a.wq_ctr = h->wq_buf;
-  a.wq_err = h->wq_buf + 16;
-  a.wq_prog = h->wq_buf + 32;
-  a.wq_ranges = (int)((nsteps + fuse - 1) / fuse);
-  a.wq_total = (int)nsteps;
-  a.wq_nxcc = h->wq_nxcc;
-  hipLaunchKernelGGL((k_fused<float, false, false, false, false, kCellsPerThread, false, true>), h->wq_blocks, kBlock,
-                     lds, h->stream, a, d_u, (const float*)h->forc, (const float*)h->stat, h->geo, h->catch_id, h->st,
-                     h->tot, h->ring, (float*)h->hist, h->slab, (const float*)h->qc);
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemcpyAsync(h->wq_err_h, h->wq_buf + 16, 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipEventRecord(h->wq_ev, h->stream));
-  ++h->wq_launches;
-  return TFG_OK;
-}
-
 int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
                  const IoArgs& io = IoArgs()) {
   if (int rc = prepare_steps(h)) return rc;
@@ -1630,20 +1524,6 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   // (see the prefetch note in k_fused)
   const int fuse = h->ring_len > (h->engine == TFG_F32 ? kPrefetchFast : 1) ? h->fuse : 1;
   const bool one_cell = h->engine == TFG_F64 && h->n == 1 && !io.in;  // k_cell_run
-  if (h->wq == 2)
-    if (int rc = wq_setup(h, lds)) return rc;
-  // TFG_WQ=1: the fp32 clean form of several launches' worth of steps as one
-  // work-queue launch (after the first launch, which reads the initial depths)
-  if (h->wq == 1 && h->engine == TFG_F32 && !io.in && !h->qc_on && !h->catch_id && h->depths_derived &&
-      nsteps > fuse && nsteps < (1ll << 30)) {
-    bool ns = true;
-    if (int rc = choose_form(h, u, (int)nsteps, io, &ns)) return rc;
-    if (!ns) {
-      if (int rc = launch_wq(h, d_u, nsteps, fuse, lds)) return rc;
-      h->last_hist = u[nsteps - 1].hist;
-      return TFG_OK;
-    }
-  }
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
     int rc = TFG_OK;
@@ -1773,7 +1653,7 @@ int tfg_sync(tfg_handle* h) {
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  return wq_check(h);
+  return TFG_OK;
 }
 
 int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_global, const float* diurnal,

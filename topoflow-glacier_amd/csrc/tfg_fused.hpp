@@ -62,17 +62,6 @@ struct KArgs {
   double* io_out;
   uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
   uint32_t io_seq;
-  // Work-queue launches (k_fused<..., WQ = true>, TFG_WQ=1): `wq_ranges` ranges
-  // of K steps (the last one shorter, wq_total steps in all) in ONE launch of
-  // resident workgroups, which pull (chunk, range) items from per-XCD counters
-  // wq_ctr[xcc]; chunk c belongs to XCD c % wq_nxcc, and wq_prog[c] counts
-  // its ranges done.  Null / 0 for every other launch.
-  int* wq_ctr = nullptr;
-  int* wq_prog = nullptr;
-  int* wq_err = nullptr;
-  int wq_ranges = 0;
-  int wq_total = 0;
-  int wq_nxcc = 0;
 };
 
 // TFG_STEP_PARAMS(p): inside a step loop, `p` names the launch's model
@@ -236,69 +225,10 @@ static __device__ unsigned long long g_wg_times[TFG_WG_TIMING][3];
 #ifndef TFG_MIN_WAVES_EXACT
 #define TFG_MIN_WAVES_EXACT 2  // fp64 engine: 256 VGPRs, no scratch spills
 #endif
-// The XCD (XCC) this wave runs on: HW_REG_XCC_ID[3:0] (a hardware-register read).
-__device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 0xF; }
-
-// Work-queue launches (KArgs::wq_*): the next (chunk, range) item of this
-// workgroup's XCD, for every thread of the workgroup.  Items are range-major,
-// so the item a range waits for, (chunk, range - 1), was taken earlier by a
-// workgroup of the same XCD that is running or done: no cycle.  The state of a
-// chunk passes from range to range through the XCD's own L2 (the one coherence
-// point its CUs share): the producer's stores have completed (vmcnt) before it
-// publishes wq_prog, and the consumer invalidates its L1 (agent-scope acquire)
-// after seeing it.  A wait is bounded: past 2^22 sleeps wq_err is set and the
-// workgroup stops (the host reports TFG_ERR_HIP).  Returns false when done.
-__device__ __forceinline__ bool wq_next(const KArgs& a, int64_t nchunks, unsigned xcc, int64_t& c, int& r) {
-  __shared__ int s_item, s_stop;
-  const int nx = a.wq_nxcc;
-  const int64_t per = (nchunks > (int64_t)xcc) ? (nchunks - (int64_t)xcc + nx - 1) / nx : 0;
-  if (threadIdx.x == 0) {
-    s_item = atomicAdd(a.wq_ctr + xcc, 1);
-    s_stop = 0;
-  }
-  __syncthreads();
-  const int item = __builtin_amdgcn_readfirstlane(s_item);  // wave-uniform: scalar registers
-  if ((int64_t)item >= per * a.wq_ranges) {
-    __syncthreads();
-    return false;
-  }
-  r = (int)(item / per);
-  c = (int64_t)xcc + (int64_t)nx * (item % per);
-  if (r > 0) {
-    if (threadIdx.x == 0) {
-      int spins = 0;
-      while (__hip_atomic_load(a.wq_prog + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < r) {
-        __builtin_amdgcn_s_sleep(8);
-        if (++spins > (1 << 22)) {
-          __hip_atomic_fetch_or(a.wq_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          s_stop = 1;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    if (s_stop) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  } else {
-    __syncthreads();
-  }
-  return true;
-}
-// The item's stores have completed (every thread), then its range is published.
-__device__ __forceinline__ void wq_done(const KArgs& a, int64_t c, int r) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(a.wq_prog + c, r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // NS (fast engine only): the NaN-safe form of the step (tfg::cell_step_fast),
 // for launches the host could not verify to read only finite values.
-// WQ: the work-queue form of a launch (KArgs::wq_*; fast engine, clean form).
-template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false, bool WQ = false>
-#ifndef TFG_MIN_WAVES_WQ
-#define TFG_MIN_WAVES_WQ 3  // the work-queue form: 143 VGPRs, no spills (at 4: 20 VGPRs spilled)
-#endif
-__global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN_WAVES_WQ : TFG_MIN_WAVES)) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false>
+__global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
                                                   const float* __restrict__ geo,   // [kGeoF][n_pad] f32 + [2][n_pad] f64
@@ -349,27 +279,10 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
 
   CellDiag acc;
   diag_zero(acc);
-  [[maybe_unused]] const unsigned wq_xcc = WQ ? xcc_id() : 0u;
-  if constexpr (WQ) {
-    if (wq_xcc >= (unsigned)a.wq_nxcc) return;  // an XCD the host's probe did not see: take no chunk
-  }
 
-  for (int64_t it = 0; WQ || it < trips; ++it) {
-    // this trip's cell groups [gb, ge), its steps (Kt) and their uniforms (ut)
-    int64_t gb = g0 + it * kBlock, ge = g1;
-    int Kt = a.K;
-    const tfg_uniforms* __restrict__ ut = uni;
-    [[maybe_unused]] int64_t wq_c = 0;
-    [[maybe_unused]] int wq_r = 0;
-    if constexpr (WQ) {
-      if (!wq_next(a, nchunks, wq_xcc, wq_c, wq_r)) break;
-      gb = wq_c * kBlock;
-      ge = std::min<int64_t>(gb + kBlock, ngroups);
-      Kt = std::min(a.K, a.wq_total - wq_r * a.K);
-      ut = uni + (int64_t)wq_r * a.K;
-    }
-    const int64_t g = gb + threadIdx.x;
-    const bool in = g < ge;
+  for (int64_t it = 0; it < trips; ++it) {
+    const int64_t g = g0 + it * kBlock + threadIdx.x;
+    const bool in = g < g1;
     int32_t cid[C];
     CellDiag cacc[CATCH ? C : 1];
     if constexpr (CATCH) {
@@ -464,7 +377,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
       // precede the write of the step before.
       struct Frame { R P[C], T[C], Q[C], PA[C], UZ[C]; int32_t q[C]; };
       auto fetch = [&](int k, Frame& f) {
-        const tfg_uniforms* un = ut + (k < Kt ? k : Kt - 1);
+        const tfg_uniforms* un = uni + (k < a.K ? k : a.K - 1);
         const R* __restrict__ fr =
             a.io_in ? static_cast<const R*>(a.io_in) : forc + (int64_t)un->frame * kNumForc * n_pad;
         static_assert(C == 1, "streamed step accesses are per cell");
@@ -481,7 +394,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
         // SGPR spills 62 -> 56 (fp32) and 170 -> 111 (fp64); same-box A/B:
         // fp32 -0.6 % and fp64 -3.4 % time per launch (HISTORY.md section 5).
         TFG_STEP_PARAMS(p);
-        const tfg_uniforms* up = ut + k;
+        const tfg_uniforms* up = uni + k;
         const tfg_uniforms u = *up;
         int32_t qn[C];
         R o_hs[C], o_sm[C], o_hi[C], o_im[C], o_mt[C], o_rh[C];
@@ -532,7 +445,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
       if constexpr (EXACT) {
         // the fp64 step is issue-bound and register-heavy: one copy of its
         // body (not two interleaved) keeps it within 256 VGPRs
-        for (int k = 0; k < Kt; ++k) {
+        for (int k = 0; k < a.K; ++k) {
           fetch(k + 1, fb);
           advance(k, fa);
           fa = fb;
@@ -541,37 +454,37 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
         Frame fc, fd;
         fetch(1, fb);
         fetch(2, fc);
-        for (int k = 0; k < Kt; k += 4) {
+        for (int k = 0; k < a.K; k += 4) {
           fetch(k + 3, fd);
           advance(k, fa);
           fetch(k + 4, fa);
-          if (k + 1 < Kt) advance(k + 1, fb);
+          if (k + 1 < a.K) advance(k + 1, fb);
           fetch(k + 5, fb);
-          if (k + 2 < Kt) advance(k + 2, fc);
+          if (k + 2 < a.K) advance(k + 2, fc);
           fetch(k + 6, fc);
-          if (k + 3 < Kt) advance(k + 3, fd);
+          if (k + 3 < a.K) advance(k + 3, fd);
         }
       } else if constexpr (kAhead == 2) {
         Frame fc;
         fetch(1, fb);
-        for (int k = 0; k < Kt; k += 3) {
+        for (int k = 0; k < a.K; k += 3) {
           fetch(k + 2, fc);
           advance(k, fa);
           fetch(k + 3, fa);
-          if (k + 1 < Kt) advance(k + 1, fb);
+          if (k + 1 < a.K) advance(k + 1, fb);
           fetch(k + 4, fb);
-          if (k + 2 < Kt) advance(k + 2, fc);
+          if (k + 2 < a.K) advance(k + 2, fc);
         }
       } else {
-        for (int k = 0; k < Kt; k += 2) {
+        for (int k = 0; k < a.K; k += 2) {
           fetch(k + 1, fb);
           advance(k, fa);
           fetch(k + 2, fa);
-          if (k + 1 < Kt) advance(k + 1, fb);
+          if (k + 1 < a.K) advance(k + 1, fb);
         }
       }
       if (a.io_in) {  // tfg_update: the frame keeps the inputs, outputs go to the host block
-        const int fidx = ut[0].frame, hidx = ut[0].hist;
+        const int fidx = uni[0].frame, hidx = uni[0].hist;
         R* __restrict__ fr = const_cast<R*>(forc) + (int64_t)fidx * kNumForc * n_pad;
         const uint32_t oR = lane_off(lc * (uint32_t)sizeof(R));
         sstore(fr + F_P * n_pad, oR, fa.P[0]);
@@ -643,7 +556,6 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : (WQ ? TFG_MIN
 #pragma unroll
       for (int j = 0; j < C; ++j) wave_flush(wbins, cid[j], cacc[j], in);
     }
-    if constexpr (WQ) wq_done(a, wq_c, wq_r);
   }
   if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
   __syncthreads();

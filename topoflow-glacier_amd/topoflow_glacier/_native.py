@@ -166,10 +166,8 @@ def code_object_sha256(path: Path | None = None) -> str | None:
     return hashlib.sha256(blob).hexdigest() if blob else None
 
 
-# k_fused<float, false, false, false, false, 1, false, false> (the last: not the work-queue form)
-BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0ELb0E"
-BENCH_KERNEL_F64 = "_ZN8tfg_kern7k_fusedIdLb1ELb0ELb0ELb0ELi1ELb0ELb0E"  # k_fused<double, true, false, false, false, 1, false, false>
-BENCH_KERNEL_WQ = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0ELb1E"  # its work-queue form (TFG_WQ=1)
+BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0E"  # k_fused<float, false, false, false, false, 1, false>
+BENCH_KERNEL_F64 = "_ZN8tfg_kern7k_fusedIdLb1ELb0ELb0ELb0ELi1ELb0E"  # k_fused<double, true, false, false, false, 1, false>
 
 
 def gfx950_code_objects(path: Path | None = None) -> list[bytes]:
