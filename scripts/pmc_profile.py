@@ -126,11 +126,13 @@ def main():
         "code_object_sha256": nat.code_object_sha256(),
         "correction": {
             "read_scale": rd_scale, "write_scale": wr_scale,
-            "source": "measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch. FETCH_SIZE "
-                      "reports half the streamed read bytes at 4 B lanes (k_fused's width) as at 16 B lanes (the "
-                      "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes"
-                      + ("" if engine == "float32" else "; fp64 engine: the 8 B and 4 B lane scales weighted by "
-                         "the algorithmic bytes of each width"),
+            "source": ("measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch. FETCH_SIZE "
+                       "reports half the streamed read bytes at 4 B lanes (k_fused's width) as at 16 B lanes (the "
+                       "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes"
+                       + ("" if engine == "float32" else "; fp64 engine: the 8 B and 4 B lane scales weighted by "
+                          "the algorithmic bytes of each width"))
+                      if cal else "not measured in this run: the defaults, FETCH_SIZE x 2 (MI355X_MICROARCH.md, gfx950) "
+                                  "and WRITE_SIZE x 1",
             "calibration": cal,
         },
         "hbm_read_bytes_per_launch": rd,
