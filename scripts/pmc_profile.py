@@ -126,9 +126,9 @@ def main():
         "code_object_sha256": nat.code_object_sha256(),
         "correction": {
             "read_scale": rd_scale, "write_scale": wr_scale,
-            "source": ("measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch. FETCH_SIZE "
-                       "reports half the streamed read bytes at 4 B lanes (k_fused's width) as at 16 B lanes (the "
-                       "width MI355X_MICROARCH.md calibrates its x2 for); WRITE_SIZE reports the bytes"
+            "source": ("measured on the same box: tools/hbm_mix cal kernels with known bytes per dispatch at 4, 8 "
+                       "and 16 B lanes (counter_over_known below); the read and write scales are the inverse of the "
+                       "measured ratios at the kernel's lane widths"
                        + ("" if engine == "float32" else "; fp64 engine: the 8 B and 4 B lane scales weighted by "
                           "the algorithmic bytes of each width"))
                       if cal else "not measured in this run: the defaults, FETCH_SIZE x 2 (MI355X_MICROARCH.md, gfx950) "
