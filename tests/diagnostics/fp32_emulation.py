@@ -11,6 +11,7 @@ log biased by -0.44 ulp), and its miss rates are a lower bound of the GPU's.
 
 `promote` switches term groups to fp64, as a kernel variant would:
   "lw"    T_K, T_surf_K and the long-wave balance in fp64 (em_air stays fp32)
+  "lwx"   the long-wave balance in fp32 without its cancellation: (em - 1) Ta^4 + dTs (Ta + Ts)(Ta^2 + Ts^2)
   "em"    em_air's power (e/T)^(1/7) in fp64
   "dew"   e_air, the dew point and T_air - T_surf in fp64
   "sum"   the flux sum and E_in in fp64
@@ -253,7 +254,16 @@ class Fp32Engine:
                 em = em.astype(f32).astype(f64)
         else:
             em = f64(fma32(self.f_ccF, exp2_32(log2_32(e_air * f32(0.1) * rT) * f32(1 / 7)), self.f_F))
-        if "lw" in pr:
+        if "lwx" in pr:
+            # fp32, without the cancellation: em Ta^4 - Ts^4 = (em - 1) Ta^4 + (Ta - Ts)(Ta + Ts)(Ta^2 + Ts^2),
+            # Ta - Ts = T_air - T_surf (dTs, in degC)
+            TsK = T_surf + f32(273.15)
+            ta2 = T_K * T_K
+            sq = fma32(T_K, T_K, TsK * TsK)
+            d4 = dTs * (T_K + TsK) * sq
+            emf = em.astype(f32)
+            Qlw64 = f64(self.f_em_s_sigma * fma32(emf - f32(1.0), ta2 * ta2, d4))
+        elif "lw" in pr:
             ta, ts = f64(T_air) + 273.15, T_surf64 + 273.15
             Qlw64 = self.em_s_sigma * (em * ta ** 4 - ts ** 4)
         else:

@@ -1009,6 +1009,9 @@ __device__ __forceinline__ double root7_d(double x) {
 #define TFG_QSUM_F64 0
 #endif
 #define TFG_ACC_SUM (((TFG_ACC) & 16) || TFG_QSUM_F64)
+#ifndef TFG_LW_SPLIT
+#define TFG_LW_SPLIT 1  // the fp32 long-wave balance without its cancellation (below)
+#endif
 
 template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
@@ -1203,6 +1206,17 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const double a2 = TK_d2 * TK_d2, s2 = tks * tks;
   const double Qn_LW_d = p.em_surf_sigma * fma(em_d, a2 * a2, -(s2 * s2));
   const float Qn_LW = (float)Qn_LW_d;
+#elif TFG_LW_SPLIT
+  // em Ta^4 - Ts^4 without its cancellation (LW_in ~ LW_out ~ 300 W m-2 net
+  // ~100): (em - 1) Ta^4 + (Ta - Ts)(Ta + Ts)(Ta^2 + Ts^2), with Ta - Ts the
+  // degC difference dTs (exact of the two fp32 sums' rounding) and em - 1 exact;
+  // the pure-relative misses of SM fall 1.6x in the fp32 emulation
+  // (tests/diagnostics/fp32_emulation.py "lwx"), as with the fp64 balance
+  const float T_surf_K = T_surf + 273.15f;
+  const float ta2 = T_K * T_K;
+  const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
+  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air - 1.0f, ta2 * ta2, d4);
+  const double Qn_LW_d = (double)Qn_LW;
 #else
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
