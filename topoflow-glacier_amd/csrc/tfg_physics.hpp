@@ -1010,7 +1010,7 @@ __device__ __forceinline__ double root7_d(double x) {
 #endif
 #define TFG_ACC_SUM (((TFG_ACC) & 16) || TFG_QSUM_F64)
 #ifndef TFG_LW_SPLIT
-#define TFG_LW_SPLIT 1  // the fp32 long-wave balance without its cancellation (below)
+#define TFG_LW_SPLIT 0  // 1: the fp32 long-wave balance without its cancellation (below)
 #endif
 
 template <bool QC, bool NANSAFE>
