@@ -29,12 +29,12 @@ int main() {
   std::uniform_real_distribution<double> u(-1.0, 1.0);
   for (int i = 0; i < n; ++i) x[i] = (float)std::exp2(u(rng) * 10.0);  // [2^-10, 2^10]
   float *dx, *dout;
-  hipMalloc(&dx, n * 4);
-  hipMalloc(&dout, 5 * n * 4);
-  hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
+  (void)hipMalloc(&dx, n * 4);
+  (void)hipMalloc(&dout, 5 * n * 4);
+  (void)hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
   k_eval<<<(n + 255) / 256, 256>>>(dx, dout, n);
   std::vector<float> out(5 * n);
-  hipMemcpy(out.data(), dout, 5 * n * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out.data(), dout, 5 * n * 4, hipMemcpyDeviceToHost);
   const char* names[5] = {"v_rcp_f32", "v_log_f32 (log2)", "v_exp_f32 (exp2)", "sqrt", "rcp + 1 Newton step"};
   for (int f = 0; f < 5; ++f) {
     double s = 0, mx = 0, su = 0;

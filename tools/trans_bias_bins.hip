@@ -20,12 +20,12 @@ int main() {
   for (int b = 0; b < bins; ++b)
     for (int j = 0; j < per; ++j) x[b * per + j] = -3.0f + 0.25f * b + 0.25f * (j + 0.5f) / per;  // [-3, 3)
   float *dx, *dout;
-  hipMalloc(&dx, n * 4);
-  hipMalloc(&dout, 3 * n * 4);
-  hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
+  (void)hipMalloc(&dx, n * 4);
+  (void)hipMalloc(&dout, 3 * n * 4);
+  (void)hipMemcpy(dx, x.data(), n * 4, hipMemcpyHostToDevice);
   k_eval<<<(n + 255) / 256, 256>>>(dx, dout, n);
   std::vector<float> out(3 * n);
-  hipMemcpy(out.data(), dout, 3 * n * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(out.data(), dout, 3 * n * 4, hipMemcpyDeviceToHost);
   for (int f = 0; f < 3; ++f) {
     std::printf("%s:", f == 0 ? "exp2(x)" : f == 1 ? "log2(x+3)" : "rcp(x+3)");
     for (int b = 0; b < bins; ++b) {
