@@ -689,7 +689,9 @@ def dropin_instances_leg(args, local: int, steps: int = 8) -> dict:
            "land_surface_air__pressure": 88000.0, "atmosphere_air_water~vapor__relative_saturation": 0.003,
            "wind_speed_UV": 3.0, "land_surface_radiation~incoming~longwave__energy_flux": 250.0,
            "land_surface_radiation~incoming~shortwave__energy_flux": 100.0}
-    vals = {k: np.array([v]) for k, v in ins.items()}
+    # numpy scalars, as the reference's driver passes them (examples/run_topoflow_glacier.py:65-73: values of
+    # pandas columns, one per step)
+    vals = {k: np.float64(v) for k, v in ins.items()}
     outs = models[0].get_output_var_names()
     buf = np.zeros(1)
     t_set = t_get = 0.0
@@ -716,8 +718,9 @@ def dropin_instances_leg(args, local: int, steps: int = 8) -> dict:
             "instance_steps_per_s": 1e6 / per, "us_set_and_update": t_set / (len(models) * steps) * 1e6,
             "us_get_incl_launch": t_get / (len(models) * steps) * 1e6, "create_s": t_create,
             "all_instances_equal": bool(same),
-            "protocol": "ensemble order: every model's 7 set_value + update() (queued), then every model's "
-                        "8 get_value (the first runs the queued steps in one k_cell_many launch)"}
+            "protocol": "ensemble order: every model's 7 set_value (numpy scalars, as the reference's driver) + "
+                        "update() (queued), then every model's 8 get_value (the first runs the queued steps in one "
+                        "k_cell_many launch)"}
 
 
 def main():

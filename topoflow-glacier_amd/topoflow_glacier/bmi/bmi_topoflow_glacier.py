@@ -522,7 +522,11 @@ class BmiTopoflowGlacier(BmiBase):
             ctx.set_value(name, src)
             hit = (None, _int(name) if ctx is self._outputs else None)
         else:
-            hit[0][:] = src
+            arr = hit[0]
+            if arr.size == 1 and isinstance(src, (float, np.floating)):
+                arr[0] = src  # one catchment, a scalar (NextGen's per-step pattern): 0.1 instead of 0.5 us
+            else:
+                arr[:] = src
         internal = hit[1]
         if internal is not None:
             self._stale.discard(internal)
@@ -545,7 +549,10 @@ class BmiTopoflowGlacier(BmiBase):
         """Copy of a variable, flattened into `dest` (reference :1810-1824)."""
         value = self.get_value_ptr(name)
         try:
-            dest[:] = value.reshape(-1)
+            if value.size == 1 and isinstance(dest, np.ndarray) and dest.size == 1:
+                dest[0] = value[0]  # one catchment: no flattened view to build
+            else:
+                dest[:] = value.reshape(-1)
         except Exception as e:
             raise RuntimeError(f"Could not return value {name} as flattened array") from e
         return dest
