@@ -16,7 +16,10 @@ footprint ~266 GB of the 288 GB: 24 forcing frames 32 GB, 128 output slots
 2^25 cells or fewer fuse 256 steps per launch (N = 2), 2^24 or fewer 384
 (N >= 4; auto_fuse).
 
---gpus N: one process per GPU (torchrun).  By default the ONE 8192 x 8192 grid
+--gpus N: one process per GPU.  Under torch.distributed.run (the driver) the
+process group must have N ranks; started bare, the bench starts the N ranks
+itself as a child torch.distributed.run and relays its line (launch_ranks).
+By default the ONE 8192 x 8192 grid
 is row-partitioned over the N ranks (strong scaling, BASELINE config 4: 1024 x
 8192 per GPU at N = 8); --scaling weak gives every rank its own --ny rows.
 There is no data-path collective; value = all cells x steps / max-over-ranks
@@ -325,14 +328,12 @@ def capture_parity(eng, args, plan: dict, world: int, torch, local: int) -> dict
     kc = max(args.catchments, 1)
     dev = torch.device("cuda", local)
     cnt = np.bincount(np.arange(1 + k) % args.frames, minlength=args.frames)
-    cid = torch.from_numpy(catchment_blocks(plan["row0"], plan["rows"], plan["ny_global"], args.nx, args.catchments)
-                           if args.catchments else np.zeros(eng.n, np.int32)).to(dev).long()
     P = torch.empty(eng.n, dtype=torch.float32 if args.engine == "float32" else torch.float64, device=dev)
     T = torch.empty_like(P)
     sums = torch.zeros((3, eng.n), dtype=torch.float64, device=dev)
-    pmax = torch.full((kc,), -float("inf"), dtype=torch.float64, device=dev)
+    pcell = torch.full((eng.n,), -float("inf"), dtype=torch.float64, device=dev)
     t_rs = BASE_CFG["T_rain_snow"]
-    for f in np.nonzero(cnt)[0]:
+    for f in np.nonzero(cnt)[0]:  # per cell first: elementwise, no two cells share an address
         eng.get_field_device("P", P, index=int(f))
         eng.get_field_device("T_air", T, index=int(f))
         p64 = P.double()
@@ -340,41 +341,39 @@ def capture_parity(eng, args, plan: dict, world: int, torch, local: int) -> dict
         sums[0] += p64 * float(cnt[f])
         sums[1] += torch.where(rain, p64, 0.0) * float(cnt[f])
         sums[2] += torch.where(rain, 0.0, p64) * float(cnt[f])
-        pmax = pmax.scatter_reduce(0, cid, p64, reduce="amax", include_self=True)
+        torch.maximum(pcell, p64, out=pcell)
+    # then per catchment as reductions, not atomics: an index_add_ / scatter_reduce of
+    # every cell into one bin serialised on that address (~68 s of a driver run at 8192^2)
+    if args.catchments:
+        cid = catchment_blocks(plan["row0"], plan["rows"], plan["ny_global"], args.nx, args.catchments)
+        order = torch.argsort(torch.from_numpy(cid).to(dev), stable=True)
+        lengths = torch.from_numpy(np.bincount(cid, minlength=kc)).to(dev)
+
+        def seg(x, how):
+            return torch.segment_reduce(x[order], how, lengths=lengths)
+    else:
+        def seg(x, how):
+            return (x.sum() if how == "sum" else x.max()).reshape(1)
     da_dt = BASE_CFG["da"] * 1e6 * args.dt
-    want = torch.stack([torch.zeros(kc, dtype=torch.float64, device=dev).index_add_(0, cid, sums[i])
-                        for i in range(3)], 1).cpu().numpy() * da_dt
+    want = torch.stack([seg(sums[i], "sum") for i in range(3)], 1).cpu().numpy() * da_dt
     return {"plan": pp, "gpu": gpu, "nan_safe_launches": ns, "diag": diag, "want_P_PR_PS": want,
-            "want_P_max": pmax.cpu().numpy()}
+            "want_P_max": seg(pcell, "max").cpu().numpy()}
 
 
-def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: dict):
-    """This rank's GPU-vs-oracle check, outside the timed region (every rank,
-    at every N): the outputs capture_parity kept from the bench handle's own
-    lead-in and first whole launch, on the first rows of this rank's shard,
-    against the numpy oracle (oracle/tfg_oracle.py, fp64, bit-exact to the
-    reference fixtures) on the host mirror of the same synthetic fp32 inputs,
-    every output at every step.  Cells whose trajectories part at a melt-out
-    residual are compared up to the flip and counted, held to the fp64
-    baseline of the same cells and steps (the C oracle against the numpy
-    oracle; tests/harness.py flip_rule).  The shard's per-catchment
-    precipitation integrals and P_max are checked against the sums of the
-    forcing it read.
-
-    Returns (parity dict, the numpy run's single-core rate as a CPU leg)."""
+def oracle_sample(args, pp: dict, threads: int):
+    """The reference side of a rank's parity check: the numpy oracle
+    (oracle/tfg_oracle.py, fp64, bit-exact to the reference fixtures) on the
+    host mirror of the synthetic fp32 inputs of parity_plan's cells (global
+    cell indices), every output and the four energy terms at every step, and
+    the C oracle (the fp64 baseline of the flip rule) on the same cells.
+    Returns (ref, c64, the numpy run as a one-core CPU leg, cfg)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import tfg_oracle as O
     import tfg_oracle_c as OC
 
-    from tests.harness import (ONSET_FRAC_MAX, depletion_steps, flip_rule, melt_onsets, melt_out_flips, scale_floor,
-                               valid_mask)
     from topoflow_glacier.synthetic import diurnal_table, synthetic_cells
 
-    pp = cap["plan"]
-    rows, nx, row0, steps = pp["rows"], args.nx, pp["row0"], pp["steps"]
-    n = pp["cells"]
-    gpu, diag, ns = cap["gpu"], cap["diag"], cap["nan_safe_launches"]
-    # (2) the numpy oracle on the host mirror of the same inputs (global cell indices)
+    rows, nx, row0, steps, n = pp["rows"], args.nx, pp["row0"], pp["steps"], pp["cells"]
     cells = ((row0 + np.arange(rows))[:, None] * nx + np.arange(nx)[None, :]).reshape(-1)
     syn = synthetic_cells(args.seed, cells, diurnal_table(args.frames))
     static = _static_of(syn)
@@ -400,26 +399,39 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
                            f"({t_np:.1f} s), the reference of the parity check"}
     note("parity: C oracle (fp64 baseline of the flip rule)")
     c64, _ = OC.run_oracle_c(cfg, static, forcing, steps, clock=(jd, tsn), frames=frames, hist=True, nthreads=threads)
+    return ref, {v: c64[v] for v in HIST}, numpy_leg, cfg
+
+
+def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: dict):
+    """This rank's GPU-vs-oracle check, outside the timed region (every rank,
+    at every N): the outputs capture_parity kept from the bench handle's own
+    lead-in and first whole launch, on the first rows of this rank's shard,
+    against the numpy oracle (oracle/tfg_oracle.py, fp64, bit-exact to the
+    reference fixtures) on the host mirror of the same synthetic fp32 inputs,
+    every output at every step.  Cells whose trajectories part at a melt-out
+    residual are compared up to the flip and counted, held to the fp64
+    baseline of the same cells and steps (the C oracle against the numpy
+    oracle; tests/harness.py flip_rule).  The shard's per-catchment
+    precipitation integrals and P_max are checked against the sums of the
+    forcing it read.
+
+    Returns (parity dict, the numpy run's single-core rate as a CPU leg)."""
+    from tests.harness import ONSET_FRAC_MAX, classify_sample, flip_rule, scale_floor
+
+    pp = cap["plan"]
+    rows, nx, row0, steps = pp["rows"], args.nx, pp["row0"], pp["steps"]
+    n = pp["cells"]
+    gpu, diag, ns = cap["gpu"], cap["diag"], cap["nan_safe_launches"]
+    ref, c64, numpy_leg, cfg = oracle_sample(args, pp, threads)
     tol = 1e-5 if args.engine == "float32" else 1e-10
-    note("parity: melt-out flips of the fp64 baseline")
-    c64 = {v: c64[v] for v in HIST}
-    ex64 = depletion_steps(c64, ref, cfg, tol)
-    flip64, genuine64 = melt_out_flips(c64, ref, tol, ex64)
+    # depletion steps (the rate carries the remaining depth's error), melt-out flips held to the fp64
+    # baseline (C oracle vs numpy oracle) and, for the fp32 engine, melt onsets (E_in - Eccs cancelling),
+    # classified as the GPU suite does (tests/harness.py classify_sample)
+    note("parity: classifying the sample")
+    cls = classify_sample(gpu, ref, c64, cfg, tol, onsets=args.engine == "float32")
     del c64
-    note("parity: melt-out flips of the GPU")
-    # the last melt of a reservoir: the rate carries the remaining depth's error (harness.depletion_steps)
-    excused = depletion_steps(gpu, ref, cfg, tol)
-    flip, genuine = melt_out_flips(gpu, ref, tol, excused)
-    # melt onset of the fp32 engine: where E_in - Eccs cancels, SM carries the fp32 flux error of all the
-    # energy moved so far; explained within 1e-6 of it in at most 0.5 % of the cells, as in the GPU suite
-    onset = {}
-    if args.engine == "float32" and genuine:
-        onset, genuine = melt_onsets(gpu, ref, genuine, cfg)
-    cut = flip.copy()
-    for c_, k_ in onset.items():
-        cut[c_] = k_
-    onset_ok = len(onset) <= int(np.ceil(ONSET_FRAC_MAX * n))
-    ok = valid_mask(cut, steps) & ~excused
+    excused, flip, genuine, onset, ok = cls.excused, cls.flip, cls.genuine, cls.onset, cls.ok
+    flip64, genuine64, ex64, onset_ok = cls.flip64, cls.genuine64, cls.ex64, cls.onset_ok
     # each output's floor s_v from the whole sample (as the classifiers take it), not the compared part
     floors = {v: scale_floor(ref[v]) for v in HIST}
     by_out = {v: _floored_rel(gpu[v][ok], ref[v][ok], floors[v])[0] for v in HIST}
@@ -723,8 +735,58 @@ def dropin_instances_leg(args, local: int, steps: int = 8) -> dict:
                         "k_cell_many launch)"}
 
 
-def main():
-    args = parse()
+def rank_launch_command(gpus: int, argv: list[str], port: int) -> list[str]:
+    """The child that runs this bench as `gpus` ranks, one process per GPU, as
+    the driver itself launches N > 1 (torch.distributed.run, 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", str(ROOT / "bench.py"), *argv]
+
+
+def launch_ranks(args, argv: list[str]) -> int | None:
+    """`--gpus N` is honoured however the bench is started.  Under a launcher
+    (WORLD_SIZE set) the process group must have N ranks: a mismatch exits 2
+    rather than print a line for another N.  Started bare with N > 1, the bench
+    runs N ranks as a CHILD process (torch.distributed.run; this process never
+    touches the GPU, so nothing is exec'd after GPU initialisation), relays
+    rank 0's one JSON line on stdout and everything else on stderr, and exits
+    with the child's code.  Returns None when this process is itself the rank."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks", file=sys.stderr)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = rank_launch_command(args.gpus, argv, port)
+    note(f"--gpus {args.gpus}: starting {args.gpus} ranks: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, cwd=str(ROOT))
+    for line in proc.stdout:
+        if line.lstrip().startswith("{"):
+            print(line.rstrip("\n"), flush=True)
+        else:
+            print(line, end="", file=sys.stderr, flush=True)
+    return proc.wait()
+
+
+def agree_on_depth(args, pg: bool, torch, dist, local: int, backend: str) -> int:
+    """Every rank fuses the same depth: the smallest any rank could allocate
+    (a rank whose tfg_create ran out of memory stepped down DEPTH_LADDER)."""
+    if not pg:
+        return args.fuse
+    t = torch.tensor([args.fuse], dtype=torch.int64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return int(t.item())
+
+
+def main(args=None):
+    args = args or parse()
     import torch
     import torch.distributed as dist
 
@@ -766,10 +828,13 @@ def main():
                               args.catchments > 0)
         if args.fuse != auto:
             depth_note = f"{auto}-step history over the {DEVICE_BYTES_BUDGET / 1e9:.0f} GB budget; fused {args.fuse} steps"
+    def create(depth: int):
+        return GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+                             hist_depth=depth, fuse_steps=depth, row0=row0, n_catch=n_catch)
+
     while True:
         try:
-            eng = GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
-                                hist_depth=args.fuse, fuse_steps=args.fuse, row0=row0, n_catch=n_catch)
+            eng = create(args.fuse)
             break
         except NativeError as e:
             # a device that cannot hold the history of the automatic depth fuses the
@@ -780,6 +845,13 @@ def main():
             depth_note = f"{args.fuse}-step history did not fit ({e}); fused {smaller[0]} steps"
             args.fuse = smaller[0]
             torch.cuda.empty_cache()
+    agreed = agree_on_depth(args, pg, torch, dist, local, backend)  # one collective, on every rank
+    if agreed != args.fuse:  # another rank stepped down: this one follows, so every rank times the same launches
+        eng.close()
+        torch.cuda.empty_cache()
+        depth_note = f"another rank could not hold {args.fuse} history slots; every rank fused {agreed} steps"
+        args.fuse = agreed
+        eng = create(agreed)
     eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
     if args.catchments > 0:
         eng.set_field("catch_id", catchment_blocks(row0, rows, ny_global, args.nx, args.catchments))
@@ -960,4 +1032,8 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    _args = parse()
+    _rc = launch_ranks(_args, sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+    main(_args)

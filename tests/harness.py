@@ -300,6 +300,30 @@ def valid_mask(flip: np.ndarray, nsteps: int) -> np.ndarray:
     return (flip[None, :] < 0) | (k < flip[None, :])
 
 
+def classify_sample(gpu: dict, ref: dict, c64: dict, cfg: dict, tol: float, onsets: bool) -> SimpleNamespace:
+    """Every rule of a parity check on one sample, as the GPU suite, smoke and
+    each bench rank apply them: depletion steps, melt-out flips (held to the
+    fp64 baseline c64 of the same cells and steps), and with `onsets` (the
+    fp32 engine) melt onsets.  Returns the per-entry compare mask `ok`
+    ([nsteps][ncell]: not excused, cell not yet cut) with the classifications."""
+    names = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
+    c64 = {v: c64[v] for v in names}
+    ex64 = depletion_steps(c64, ref, cfg, tol)
+    flip64, genuine64 = melt_out_flips(c64, ref, tol, ex64)
+    excused = depletion_steps(gpu, ref, cfg, tol)
+    flip, genuine = melt_out_flips(gpu, ref, tol, excused)
+    onset = {}
+    if onsets and genuine:
+        onset, genuine = melt_onsets(gpu, ref, genuine, cfg)
+    cut = flip.copy()
+    for c_, k_ in onset.items():
+        cut[c_] = k_
+    nsteps, ncell = np.asarray(ref["SM"]).shape
+    return SimpleNamespace(excused=excused, flip=flip, genuine=genuine, onset=onset, cut=cut,
+                           ok=valid_mask(cut, nsteps) & ~excused, ex64=ex64, flip64=flip64, genuine64=genuine64,
+                           onset_ok=len(onset) <= int(np.ceil(ONSET_FRAC_MAX * ncell)))
+
+
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
                 fuse_steps: int = 24, row0: int = 0):
     from topoflow_glacier.engine import GlacierEngine

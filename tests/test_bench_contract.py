@@ -201,6 +201,73 @@ def test_bench_parity_holds_at_the_deep_launches_of_the_multi_gpu_lines():
     assert sp["max_floored_rel"] <= sp["tolerance"] and sp["ok"], sp["max_floored_rel_at"]
 
 
+def test_gpus_flag_starts_its_ranks_as_a_child(monkeypatch, capsys):
+    """`python bench.py --gpus N` run bare (no WORLD_SIZE) starts N ranks as a
+    child torch.distributed.run on 127.0.0.1 with the same arguments, relays
+    rank 0's JSON line on stdout (anything else on stderr) and returns the
+    child's exit code; --gpus 1 and a launcher's own rank run inline."""
+    import io
+    import subprocess as sp
+
+    bench, args = _args("--gpus", "4", "--steps", "20", "--warmup", "5")
+    seen = {}
+
+    class FakeChild:
+        def __init__(self, cmd, **kw):
+            seen["cmd"], seen["kw"] = cmd, kw
+            self.stdout = io.StringIO('warning from a rank\n{"n_gpus": 4}\n')
+
+        def wait(self):
+            return 7
+
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sp, "Popen", FakeChild)
+    rc = bench.launch_ranks(args, ["--gpus", "4", "--steps", "20", "--warmup", "5"])
+    cmd = seen["cmd"]
+    assert rc == 7 and cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=4" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert any(a.startswith("--master-port=") for a in cmd)
+    assert cmd[-7:] == [str(ROOT / "bench.py"), "--gpus", "4", "--steps", "20", "--warmup", "5"]
+    out = capsys.readouterr()
+    assert out.out.strip() == '{"n_gpus": 4}' and "warning from a rank" in out.err
+    # inline: one GPU, or already a rank of a launcher whose size matches
+    _, one = _args("--gpus", "1")
+    assert bench.launch_ranks(one, []) is None
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.launch_ranks(args, []) is None
+
+
+def test_gpus_flag_refuses_a_launcher_of_another_size():
+    """Under a launcher whose WORLD_SIZE differs from --gpus the bench exits 2
+    before importing torch, instead of printing a line for another N."""
+    import os
+
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE=3" in r.stderr and r.stdout == ""
+
+
+@pytest.mark.gpu
+def test_bare_gpus_two_runs_two_ranks():
+    """`python3 bench.py --gpus 2 ...` with no launcher around it: the bench
+    starts its two ranks itself (here both on the one GPU of the box, over
+    gloo) and prints one line with n_gpus 2 and a world-2 process group."""
+    import os
+
+    env = dict(os.environ, TFG_BENCH_ONE_DEVICE="1", TFG_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--ny", "512", "--nx", "1024", "--steps", "48",
+           "--warmup", "24", "--fuse", "24"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["process_group"] == {"backend": "gloo", "world_size": 2}
+    assert [x["rows"] for x in d["ranks"]["ranks"]] == [256, 256] and d["sample_parity"]["ok"]
+
+
 def test_rank_report_names_the_devices_and_the_slowest_rank():
     """The per-rank record a multi-GPU line carries (bench.rank_report): ranks
     in order, the slowest one, max/min span, distinct GPUs; two RCCL ranks on

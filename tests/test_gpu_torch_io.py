@@ -51,3 +51,28 @@ def test_set_field_from_a_fresh_torch_tensor():
             assert np.array_equal(e.get_field("T_air", index=f, dtype=np.float32), want), f
     finally:
         e.close()
+
+
+def test_set_inputs_from_a_dropped_tensor_on_the_engines_own_stream():
+    """tfg_set_inputs from a device tensor reads it asynchronously on the
+    engine's own stream: the tensor is recorded on that stream, so dropping it
+    at once and letting torch refill the freed block cannot change what the
+    engine reads (GlacierEngine.set_inputs)."""
+    import torch
+
+    e = make_engine(BASE_CFG, NY, NX, "float32", n_frames=2, hist_depth=1)
+    try:
+        torch.cuda.synchronize()
+        for f in range(2):
+            x = torch.arange(5 * NY * NX, dtype=torch.float32, device="cuda:0").reshape(5, NY * NX) * 1e-3 + f
+            e.set_inputs(x, index=f)  # BMI order P_air, Hum_sp, P, T_air, uz
+            del x
+            junk = torch.full((5, NY * NX), -7.0, dtype=torch.float32, device="cuda:0")  # the freed block, if reused
+            del junk
+            want = np.arange(5 * NY * NX, dtype=np.float32).reshape(5, NY * NX) * np.float32(1e-3) + np.float32(f)
+            for row, name in enumerate(("P_air", "Hum_sp", "P", "T_air", "uz")):
+                assert np.array_equal(e.get_field(name, index=f, dtype=np.float32), want[row]), (name, f)
+        with pytest.raises(ValueError):
+            e.set_inputs(torch.zeros((5, NY * NX - 1), dtype=torch.float32, device="cuda:0"))
+    finally:
+        e.close()

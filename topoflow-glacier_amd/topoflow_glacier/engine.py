@@ -177,21 +177,29 @@ class GlacierEngine:
     def set_inputs(self, values, index: int = 0) -> None:
         """The five physics inputs of one frame in one call: values [5][n] in
         BMI order P_air, Hum_sp, P, T_air, uz (tfg_set_inputs): a host array,
-        or a contiguous float32 / float64 torch CUDA tensor, which the engine
-        reads on its own stream (ordered after torch's current stream when the
-        two differ; the caller keeps the tensor alive until the step has run
-        or the engine is synced)."""
+        or a contiguous float32 / float64 torch CUDA tensor on the engine's
+        device, which the engine reads asynchronously on its own stream
+        (ordered after torch's current stream when the two differ).  The read
+        is recorded on the engine's stream (Tensor.record_stream), so torch's
+        caching allocator does not hand the memory out again before the engine
+        has read it, even if the caller drops the tensor at once."""
         if getattr(values, "is_cuda", False):
             import torch
 
+            if values.device.index != self.device:
+                raise ValueError(f"inputs on {values.device}, the engine runs on cuda:{self.device}")
             if tuple(values.shape) != (5, self.n) or not values.is_contiguous():
                 raise ValueError(f"inputs must be a contiguous [5][{self.n}] tensor")
             code = {torch.float32: nat.F32, torch.float64: nat.F64}[values.dtype]
             own = getattr(self, "_stream_ptr", None)
-            same = own is not None and own == torch.cuda.current_stream(values.device).cuda_stream
-            if not same:
-                torch.cuda.current_stream(values.device).synchronize()
+            cur = torch.cuda.current_stream(values.device)
+            if own is None or own != cur.cuda_stream:
+                cur.synchronize()
             self._chk(self.lib.tfg_set_inputs(self.h, int(index), ctypes.c_void_p(values.data_ptr()), code, self.n, 1))
+            ptr = own or self.stream()
+            if getattr(self, "_ext_stream", (None, None))[0] != ptr:
+                self._ext_stream = (ptr, torch.cuda.ExternalStream(ptr, device=values.device))
+            values.record_stream(self._ext_stream[1])
             return
         a = np.ascontiguousarray(values, dtype=np.float64)
         if a.shape != (5, self.n):
