@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 5
+#define TFG_ABI_VERSION 6
 
 /* status codes */
 enum {
@@ -280,9 +280,16 @@ int tfg_sync(tfg_handle* h);
  * stream-ordered (no host wait) and of unknown status; before a launch of 8
  * or more steps unknown data is checked (a synchronous device check), and a
  * shorter launch runs the NaN-safe form.  *count = launches that ran the
- * NaN-safe form.
- * The environment variable TFG_NANSAFE=1 at tfg_create forces that form. */
+ * NaN-safe form. */
 int tfg_nan_safe_launches(tfg_handle* h, int64_t* count);
+
+/* The fp32 engine's step form: TFG_FORM_AUTO (the default: chosen per launch
+ * as above) or TFG_FORM_NAN_SAFE (every launch; the same results wherever the
+ * data is finite -- tests and measurements of the two forms).  No reference
+ * counterpart. */
+#define TFG_FORM_AUTO 0
+#define TFG_FORM_NAN_SAFE 1
+int tfg_set_step_form(tfg_handle* h, int form);
 
 /* Self-test of the fp64 engine's power rewrites on the device (tests only):
  * out[i] = pow4(x[i]) (which = 0: T^4, :1231-1233), pow1p5(x[i]) (1: RH^1.5,

@@ -272,33 +272,36 @@ def test_satterlund_synthetic_vs_oracle():
 
 # ---------------------------------------------------------------- invariances
 @pytest.mark.parametrize("engine", ["float32", "float64"])
-def test_plane_stride_is_invisible(engine, monkeypatch):
+def test_plane_stride_is_invisible(engine):
     """Shards of 2^20 cells or more get a plane stride of n + 512 cells
-    (tfg_create, kPlaneSkew); the padding changes no result: a 1024 x 1024
-    shard with the default stride, with TFG_PLANE_SKEW=0 and with a 4096-cell
-    skew gives the same outputs, state and diagnostics bit for bit."""
-    runs = []
-    for skew in (None, "0", "4096"):
-        if skew is None:
-            monkeypatch.delenv("TFG_PLANE_SKEW", raising=False)
-        else:
-            monkeypatch.setenv("TFG_PLANE_SKEW", skew)
-        e = make_engine(BASE_CFG, 1024, 1024, engine, n_frames=24, hist_depth=24, fuse_steps=24)
+    (tfg_create, kPlaneSkew), smaller ones none; the padding changes no
+    result: one 1024 x 1024 shard (skewed stride) gives the same outputs,
+    state and diagnostics bit for bit as its two 512-row halves (unskewed),
+    each run as its own shard of the same global cells."""
+    def run(ny, row0):
+        e = make_engine(BASE_CFG, ny, 1024, engine, n_frames=24, hist_depth=24, fuse_steps=24, row0=row0)
         try:
-            e.fill_synthetic(5, synthetic_inputs(5, 1, 1, 24)[1])
+            e.fill_synthetic(5, synthetic_inputs(5, 1, 1, 24)[1], nx_global=1024)
             e.run(48)
             e.sync()
             outs = {v: np.stack([e.get_field(v, index=k) for k in range(24)]) for v in HIST}
             state = {v: e.get_field(v) for v in ("h_swe", "h_iwe", "Eccs", "Ecci", "albedo", "n")}
-            runs.append((outs, state, e.diagnostics()))
+            return outs, state, e.diagnostics()
         finally:
             e.close()
-    for o, st, dg in runs[1:]:
-        for v in HIST:
-            assert np.array_equal(o[v], runs[0][0][v]), v
-        for v in st:
-            assert np.array_equal(st[v], runs[0][1][v]), v
-        assert np.array_equal(dg, runs[0][2])
+
+    whole = run(1024, 0)
+    halves = [run(512, 0), run(512, 512)]
+    for v in HIST:
+        assert np.array_equal(whole[0][v], np.concatenate([h[0][v] for h in halves], axis=1)), v
+    for v in whole[1]:
+        assert np.array_equal(whole[1][v], np.concatenate([h[1][v] for h in halves])), v
+    for c in (0, 1, 2, 5):  # the precipitation integrals and P_max are exact sums / maxima of the forcing
+        want = max(h[2][0, c] for h in halves) if c == 5 else None
+        if c == 5:
+            assert whole[2][0, c] == want
+        else:
+            assert abs(whole[2][0, c] - sum(h[2][0, c] for h in halves)) <= 1e-12 * abs(whole[2][0, c])
 
 
 @pytest.mark.parametrize("engine", ["float32", "float64"])
@@ -902,23 +905,20 @@ def test_checkpoint_restart_is_bit_exact(tmp_path, engine):
         np.testing.assert_array_equal(runs[1][k], runs[0][k], err_msg=k)
 
 
-def test_fp32_step_forms_agree_on_finite_data_and_the_engine_picks_them(monkeypatch):
+def test_fp32_step_forms_agree_on_finite_data_and_the_engine_picks_them():
     """The fp32 engine's two step forms (tfg_physics.hpp, "Missing data"): on
     finite data the NaN-safe form equals the clean form bit for bit (outputs,
     state, window slots, diagnostics).  A finite run takes the clean form in
     every launch; a NaN in one forcing frame sends the launches that read it,
     and (through the state it leaves) the launches after, to the NaN-safe form;
-    TFG_NANSAFE=1 forces it everywhere."""
+    tfg_set_step_form(TFG_FORM_NAN_SAFE) forces it everywhere."""
     g = load_golden("grid64")
     nsteps = 100
     runs = {}
     for mode in ("clean", "forced"):
-        if mode == "forced":
-            monkeypatch.setenv("TFG_NANSAFE", "1")
-        else:
-            monkeypatch.delenv("TFG_NANSAFE", raising=False)
         e = make_engine(g["cfg"], 8, 8, "float32", n_frames=nsteps, hist_depth=nsteps, fuse_steps=24)
         try:
+            e.set_step_form(mode == "forced")
             for k in ("elev", "slope", "aspect"):
                 e.set_field(k, g["static"][k])
             for k in ("h_snow", "h_ice", "h_swe", "h_iwe"):
@@ -945,7 +945,6 @@ def test_fp32_step_forms_agree_on_finite_data_and_the_engine_picks_them(monkeypa
     np.testing.assert_array_equal(da, db)
     # a NaN in frame 30: launches 0 (steps 0-23) clean, 1 (24-47) NaN-safe; then
     # the state is checked before each launch and holds the NaN for good
-    monkeypatch.delenv("TFG_NANSAFE", raising=False)
     e = make_engine(g["cfg"], 8, 8, "float32", n_frames=nsteps, hist_depth=nsteps, fuse_steps=24)
     try:
         for k in ("elev", "slope", "aspect"):

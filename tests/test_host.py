@@ -186,7 +186,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 17
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.tfg_abi_version() == _native.ABI_VERSION == 5
+    assert L.tfg_abi_version() == _native.ABI_VERSION == 6
     assert b"gfx950" in L.tfg_build_info()
 
 
@@ -379,13 +379,14 @@ def test_library_is_built_from_these_sources():
 def test_pmc_provenance_follows_the_timed_kernel_only(tmp_path):
     """bench.py quotes PMC traffic by the timed kernel's own machine code
     (_native.kernel_code_sha256).  A build that changes only another kernel
-    (the ice-flow prefetch variant) changes the library's device code but not
-    that hash; a build that changes k_fused's stores changes it."""
+    (the one-cell kernels' phase-timing diagnostic build) changes the
+    library's device code but not that hash; a build that changes k_fused (its
+    per-workgroup timing diagnostic build) changes it."""
     import __graft_entry__ as G
     from topoflow_glacier import _native
 
-    other = G.build_engine(["-DTFG_FLOW_PF2"], out=tmp_path / "flow.so", verbose=False)
-    mine = G.build_engine(["-DTFG_NT_STORE=0"], out=tmp_path / "nt.so", verbose=False)
+    other = G.build_engine(["-DTFG_CELL_TIMING"], out=tmp_path / "cell.so", verbose=False)
+    mine = G.build_engine(["-DTFG_WG_TIMING=8"], out=tmp_path / "wgt.so", verbose=False)
     assert _native.code_object_sha256(other) != _native.code_object_sha256()
     assert _native.kernel_code_sha256(path=other) == _native.kernel_code_sha256()
     assert _native.kernel_code_sha256(path=mine) != _native.kernel_code_sha256()

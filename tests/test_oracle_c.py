@@ -136,39 +136,55 @@ def test_c_oracle_resumes_from_a_numpy_oracle_state():
         assert np.max(_floored(c[v][0], r[v])) <= RTOL, v
 
 
-def test_depletion_step_rule_holds_the_last_melt_to_the_depth_tolerance():
+def test_depletion_step_rule_checks_the_last_melt_by_the_depth_identity():
     """tests.harness.depletion_steps: at the step a snowpack runs dry in both
-    runs, SM (and M_total) carry the remaining depth's error and are held to the
-    depth's floored tolerance, not the rate's; the same mismatch with snow left
-    in either run, or a melted amount beyond the depth tolerance, stays a
-    genuine mismatch.  (The driver's 384-step launches reach such steps:
-    bench.py sample_parity)"""
+    runs, SM*3600*w_s is the depth left at the step before (update_swe caps the
+    melt, :1594-1606), so the rate's difference must equal the previous depth's
+    difference (to the rounding of the output slots).  Such an entry is marked
+    whether or not it is within the rate's own tolerance; a rate that breaks
+    the identity, or snow left in one run, is not (the rule no
+    longer excuses anything up to the depth's tolerance).  (The driver's
+    384-step launches reach such steps: bench.py sample_parity, DESIGN.md
+    section 3.)"""
     from tests.harness import BASE_CFG, depletion_steps
 
     nsteps, ncell = 4, 4000
     rng = np.random.default_rng(3)
+    ws = 1000.0 / 50.0  # rho_H2O / rho_snow (config defaults)
     ref = {v: np.zeros((nsteps, ncell)) for v in OUT_NAMES}
     ref["h_snow"][:] = rng.uniform(1.0, 6.0, (1, ncell))  # p99 floor ~6 m of snow
     ref["SM"][:] = rng.uniform(1e-7, 1e-6, (1, ncell))
     ref["h_ice"][:] = 2.0
     ref["RH"][:] = 0.5
-    c = 7
-    ref["h_snow"][1, c], ref["h_snow"][2:, c] = 0.0038, 0.0  # runs dry at step 2
-    ref["SM"][2, c] = 5.3e-8
+    c, c2 = 7, 8
+    for cc in (c, c2):
+        ref["h_snow"][1, cc], ref["h_snow"][2:, cc] = 0.0038, 0.0  # runs dry at step 2
+        ref["SM"][2, cc] = 0.0038 / (3600.0 * ws)
     ref["M_total"][:] = ref["SM"]
     gpu = {v: a.copy() for v, a in ref.items()}
-    gpu["h_snow"][1, c] = 0.00384  # 4e-5 m more snow left one step before: within the depth tolerance
-    gpu["SM"][2, c] = ref["SM"][2, c] + 3.7e-11  # ~1e-4 of the rate, 4.4e-7 m of snow
-    gpu["M_total"][2, c] = gpu["SM"][2, c]
+    d_sm = 3.7e-11  # ~1e-5 of the rate's p99 floor: out of the rate's tolerance
+    gpu["h_snow"][1, c] += d_sm * 3600.0 * ws  # the depth left one step before differs by exactly that melt
+    gpu["SM"][2, c] += d_sm
+    gpu["h_snow"][1, c2] += 1e-12 * 3600.0 * ws  # in the rate's tolerance: marked too, by the same identity
+    gpu["SM"][2, c2] += 1e-12
+    gpu["M_total"][:] = gpu["SM"]
     ex = depletion_steps(gpu, ref, BASE_CFG, 1e-5)
-    assert ex[2, c] and ex.sum() == 1
+    assert ex[2, c] and ex[2, c2] and ex.sum() == 2
     flip, genuine = melt_out_flips(gpu, ref, 1e-5, ex)
     assert not genuine and (flip < 0).all()
     assert melt_out_flips(gpu, ref, 1e-5)[1]  # without the rule: genuine
     g2 = {v: a.copy() for v, a in gpu.items()}
-    g2["SM"][2, c] = ref["SM"][2, c] + 1e-8  # 1.2e-4 m of snow: beyond the depth tolerance
+    g2["SM"][2, c] += 2 * d_sm  # the rate no longer matches the depth it melted: a defect in the capping
     g2["M_total"][2, c] = g2["SM"][2, c]
     assert not depletion_steps(g2, ref, BASE_CFG, 1e-5)[2, c]
+    assert melt_out_flips(g2, ref, 1e-5, depletion_steps(g2, ref, BASE_CFG, 1e-5))[1]
+    g4 = {v: a.copy() for v, a in gpu.items()}
+    g4["M_total"][2, c] += d_sm  # M_total is not SM + IM
+    assert not depletion_steps(g4, ref, BASE_CFG, 1e-5)[2, c]
     g3 = {v: a.copy() for v, a in gpu.items()}
-    g3["h_snow"][2, c] = 1e-12  # snow left in one run: a melt-out flip's business, not a depletion
+    g3["h_snow"][2, c] = 2e-7  # snow left in one run: not a depletion step
     assert not depletion_steps(g3, ref, BASE_CFG, 1e-5)[2, c]
+    g5 = {v: a.copy() for v, a in gpu.items()}
+    g5["h_snow"][2:, c] = 1e-19  # a melt-out residual in one run: the zero gates part there (a flip at step 2)
+    flip5, _ = melt_out_flips(g5, ref, 1e-5, depletion_steps(g5, ref, BASE_CFG, 1e-5))
+    assert flip5[c] == 2

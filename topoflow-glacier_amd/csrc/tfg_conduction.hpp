@@ -122,13 +122,9 @@ __device__ __forceinline__ void cond_lds_barrier() { asm volatile("s_waitcnt lgk
 // Tiles of kCondTX threads over kCondOut = kCondTX - 2 output columns (one
 // overlapping column each side supplies the west/east neighbours) and
 // kCondRows rows.
-#ifndef TFG_COND_ROWS
-#define TFG_COND_ROWS 64
-#endif
-#ifndef TFG_COND_AHEAD
-#define TFG_COND_AHEAD 2  // rows requested beyond the next one while a row is evaluated (1 or 2; 2: 510 against 514-516 us at 8192^2, HISTORY.md section 6)
-#endif
-constexpr int kCondTX = 256, kCondOut = kCondTX - 2, kCondRows = TFG_COND_ROWS;
+// Two rows are requested beyond the next one while a row is evaluated (one:
+// 514-516 against 510 us at 8192^2, HISTORY.md section 6).
+constexpr int kCondTX = 256, kCondOut = kCondTX - 2, kCondRows = 64;
 
 // Qc of a row-block shard.  Each thread walks down one column of its tile with
 // the rows above and below in registers and the row after next already in
@@ -158,17 +154,11 @@ __global__ __launch_bounds__(kCondTX) void k_conduction(const CondGrid g, const 
   CondCell up = cond_cell(g, cond_fetch(g, r0 - 1, cl), col_in);
   CondCell cur = cond_cell(g, cond_fetch(g, r0, cl), col_in);
   CondRaw nxt = cond_fetch(g, r0 + 1, cl);
-#if TFG_COND_AHEAD == 2
   CondRaw nx2 = cond_fetch(g, r0 + 2 < r1 ? r0 + 2 : r1, cl);
-#endif
   for (int64_t r = r0; r < r1; ++r) {
     const int b = (int)(r - r0) & 1;
     // rows past the strip re-read row r1 (a cache hit)
-#if TFG_COND_AHEAD == 2
     const CondRaw ahead = cond_fetch(g, r + 3 < r1 ? r + 3 : r1, cl);
-#else
-    const CondRaw ahead = cond_fetch(g, r + 2 < r1 ? r + 2 : r1, cl);
-#endif
     const CondCell dn = cond_cell(g, nxt, col_in);
     sC[b][0][t] = cur.Ts;
     sC[b][1][t] = cur.hs;
@@ -185,12 +175,8 @@ __global__ __launch_bounds__(kCondTX) void k_conduction(const CondGrid g, const 
     if (writes) qc[r * g.nx + c] = (R)((qs + qi) + K.qg);
     up = cur;
     cur = dn;
-#if TFG_COND_AHEAD == 2
     nxt = nx2;
     nx2 = ahead;
-#else
-    nxt = ahead;
-#endif
   }
 }
 

@@ -606,7 +606,6 @@ struct tfg_handle {
   int64_t* tot = nullptr;
   int32_t* ring = nullptr;
   void* hist = nullptr;
-  void* arena = nullptr;         // one allocation holding forc, ring and hist (TFG_ARENA), or null
   double* diag = nullptr;        // [n_catch][6]
   double* slab = nullptr;        // [max_blocks][n_catch][6]
   float* d_diurnal = nullptr;
@@ -665,7 +664,7 @@ struct tfg_handle {
   uint8_t qc_state = 1;              // the Qc plane while the conduction term is on
   int state_recheck = 0;             // launches before a dirty state is checked again
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
-  bool force_ns = false;             // TFG_NANSAFE=1: every launch NaN-safe (tests)
+  bool force_ns = false;             // tfg_set_step_form(TFG_FORM_NAN_SAFE): every launch NaN-safe
   std::string err;
 };
 
@@ -866,6 +865,21 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.f_T0 = (float)q.T0;
   p.f_c_eccs = (float)(p.rho_snow_Cp_snow * q.dt * p.ws);
   p.inv_z0 = 1.0 / q.z0_air;
+  {
+    const int k = (int)std::lround(std::log2(0.7 * p.z / q.z0_air));  // (z - h)/z0 near 2^k for h ~ 0.3 z
+    p.f_inv_z0s = (float)std::ldexp(1.0 / q.z0_air, -k);
+    p.f_l2k = (float)k;
+    p.f_l2k2 = (float)(2 * k);
+    p.f_l2kk = (float)(k * k);
+    p.f_l2min = (float)std::ldexp(0.01, -k);
+  }
+  p.f_em_sc = 102.4f;  // 0.1 * 2^10
+  p.f_ccFs = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0));
+  p.f_Fm1 = (float)(q.canopy_factor - 1.0);
+  p.f_eps100_lo = (float)(100.0 * q.eps - (double)p.f_eps100);
+  p.f_ome100_lo = (float)(100.0 * (1.0 - q.eps) - (double)p.f_ome100);
+  p.f_c6_hi = (float)(1.0 / 6.1121);
+  p.f_c6_lo = (float)(1.0 / 6.1121 - (double)p.f_c6_hi);
 }
 
 void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {
@@ -1029,10 +1043,8 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // allocations of one 4096^2 shard in one process, 113.8-116.0 with 512 cells
   // (2 KB) of skew; 1024 x 8192: 111.9-114.1 against 113.7-115.2; 8192^2:
   // 116.4-117.4 against 117.2-117.5 (tests/diagnostics/alloc_variance.py,
-  // HISTORY.md section 5).  TFG_PLANE_SKEW=<cells> overrides it (measurement).
-  int64_t skew = h->n_pad >= ((int64_t)1 << 20) ? kPlaneSkew : 0;
-  if (const char* e = std::getenv("TFG_PLANE_SKEW")) skew = round_up(std::max<int64_t>(0, atoll(e)), 64);
-  h->n_pad += skew;
+  // HISTORY.md section 5).
+  h->n_pad += h->n_pad >= ((int64_t)1 << 20) ? kPlaneSkew : 0;
   if (h->n_pad * 8 >= (int64_t)1 << 32) {
     h->err = "shard too large: ny*nx must stay below 2^29 cells per device (32-bit field offsets)";
     g_err = h->err;
@@ -1068,12 +1080,9 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // a power of two: with many catchments a slab-capped odd count (31775 at 44
   // catchments) measured 10 % slower than 32768 or 16384 (A/B, same box)
   while (h->max_blocks & (h->max_blocks - 1)) h->max_blocks &= h->max_blocks - 1;
-  if (const char* e = std::getenv("TFG_BLOCKS")) h->max_blocks = std::max(1, atoi(e));
   // no more workgroups (slab rows) than the grid has chunks: a one-cell BMI
   // handle keeps one row, not 32768 (NextGen may hold thousands of handles)
   h->max_blocks = (int)std::min<int64_t>(h->max_blocks, (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);
-  if (const char* e = std::getenv("TFG_FUSE")) h->fuse = std::max(1, atoi(e));
-  if (const char* e = std::getenv("TFG_NANSAFE")) h->force_ns = atoi(e) != 0;
   if (hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking) != hipSuccess) { h->err = "stream create failed"; return bail(TFG_ERR_HIP); }
   h->stream = h->own_stream;
   const int64_t np = h->n_pad;
@@ -1091,24 +1100,7 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
       {(void**)&h->slab, (size_t)h->max_blocks * n_catch * 6 * 8},
       {(void**)&h->d_flag, (size_t)n_frames * kNumForc * 4},  // a flag per forcing plane (choose_form)
   };
-  // TFG_ARENA=1 (measurement switch): the streamed planes -- forcing frames,
-  // window slots and output slots -- in one allocation, so that their
-  // relative placement is fixed by the layout rather than by the allocator.
-  if (const char* e = std::getenv("TFG_ARENA"); e && atoi(e) != 0) {
-    const size_t fb = (size_t)n_frames * kNumForc * np * rs, rb = (size_t)p->ring_len * np * 4,
-                 hb = (size_t)hist_depth * kNumHist * np * rs;
-    hipError_t err = hipMalloc(&h->arena, fb + rb + hb);
-    if (err != hipSuccess) {
-      h->err = std::string("hipMalloc(") + std::to_string(fb + rb + hb) + " B) failed: " + hipGetErrorString(err);
-      return bail(TFG_ERR_HIP);
-    }
-    if (hipMemsetAsync(h->arena, 0, fb + rb + hb, h->stream) != hipSuccess) { h->err = "hipMemset failed"; return bail(TFG_ERR_HIP); }
-    h->forc = h->arena;
-    h->ring = reinterpret_cast<int32_t*>(static_cast<char*>(h->arena) + fb);
-    h->hist = static_cast<char*>(h->arena) + fb + rb;
-  }
   for (auto& a : allocs) {
-    if (*a.p) continue;  // placed in the arena
     hipError_t e = hipMalloc(a.p, a.bytes);
     if (e != hipSuccess) {
       h->err = std::string("hipMalloc(") + std::to_string(a.bytes) + " B) failed: " + hipGetErrorString(e);
@@ -1128,11 +1120,6 @@ int tfg_destroy(tfg_handle* h) {
   // work queued on a caller's stream (tfg_set_stream) may still use the buffers
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
-  if (h->arena) {  // forc, ring and hist are views into it
-    (void)hipFree(h->arena);
-    h->arena = h->forc = h->hist = nullptr;
-    h->ring = nullptr;
-  }
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
                   h->flow_halo, h->flow_edges, h->flow_red, h->qc, h->cond_halo, h->cond_edges,
                   h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
@@ -1192,6 +1179,12 @@ int tfg_get_stream(tfg_handle* h, void** stream) {
 int tfg_set_fuse(tfg_handle* h, int k) {
   if (!h || k < 1) return fail(h, TFG_ERR_ARG, "fuse must be >= 1");
   h->fuse = k;
+  return TFG_OK;
+}
+
+int tfg_set_step_form(tfg_handle* h, int form) {
+  if (!h || (form != TFG_FORM_AUTO && form != TFG_FORM_NAN_SAFE)) return fail(h, TFG_ERR_ARG, "form must be TFG_FORM_AUTO or TFG_FORM_NAN_SAFE");
+  h->force_ns = form == TFG_FORM_NAN_SAFE;
   return TFG_OK;
 }
 
@@ -1402,11 +1395,7 @@ int check_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
 // The launches of nsteps steps whose uniforms the device reads at d_u (u is
 // the host copy of the same records).
 int fused_blocks(const tfg_handle* h) {
-#if TFG_STEP_SKEW
-  const int64_t ngroups = h->n_pad / kCellsPerThread;
-#else
-  const int64_t ngroups = round_up(h->n, 64) / kCellsPerThread;  // k_fused's cells only
-#endif
+  const int64_t ngroups = h->n_pad / kCellsPerThread;  // k_fused steps the whole plane stride
   return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
 }
 

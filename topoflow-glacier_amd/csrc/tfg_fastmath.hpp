@@ -65,19 +65,13 @@
 #define TFG_FM_NO_CONTRACT
 #endif
 
-// TFG_FM_SGPR_CONST=0 (A/B switch) leaves the placement of the constants of
-// log_k and exp_ks to the compiler (plain FMAs, the same results; for log_k
-// alone measured equal speed, profiles/r3f_ab_f64.log).
-#ifndef TFG_FM_SGPR_CONST
-#define TFG_FM_SGPR_CONST 1
-#endif
 
 namespace tfg_fm {
 
 // d = a * b + c with b (fma_vsv) or c (fma_vvs) a wave-uniform constant held in
 // an SGPR pair.  Host: std::fma.
 TFG_FM_HD inline double fma_vsv(double a, double b, double c) {
-#if defined(__HIP_DEVICE_COMPILE__) && TFG_FM_SGPR_CONST
+#if defined(__HIP_DEVICE_COMPILE__)
   double d;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
   return d;
@@ -86,7 +80,7 @@ TFG_FM_HD inline double fma_vsv(double a, double b, double c) {
 #endif
 }
 TFG_FM_HD inline double fma_vvs(double a, double b, double c) {
-#if defined(__HIP_DEVICE_COMPILE__) && TFG_FM_SGPR_CONST
+#if defined(__HIP_DEVICE_COMPILE__)
   double d;
   asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
   return d;
@@ -153,7 +147,7 @@ TFG_FM_HD inline double exp_impl(double x) {
   return z;
 }
 TFG_FM_HD inline double exp_k(double x) { return exp_impl<false>(x); }
-TFG_FM_HD inline double exp_ks(double x) { return exp_impl<TFG_FM_SGPR_CONST != 0>(x); }
+TFG_FM_HD inline double exp_ks(double x) { return exp_impl<true>(x); }
 
 // ---------------------------------------------------------------------------
 // log: fdlibm e_log.c's reduction and polynomial (Lg1..Lg7), one formula for

@@ -83,13 +83,8 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // DMAX: instead of stepping, the largest face diffusivity of the workgroup's
 // faces goes to out[workgroup] (the CFL bound of tfg_ice_flow_dmax).
-#ifndef TFG_FLOW_ROWS
-#define TFG_FLOW_ROWS 32
-#endif
-#ifndef TFG_FLOW_WAVES
-#define TFG_FLOW_WAVES 1  // __launch_bounds__ minimum waves per SIMD
-#endif
-constexpr int kFlowTX = 256, kFlowRows = TFG_FLOW_ROWS;  // 16 and 64 rows measured no better / slower
+constexpr int kFlowTX = 256, kFlowRows = 32;  // 16 and 64 rows measured no better / slower
+constexpr int kFlowWaves = 1;  // __launch_bounds__ minimum waves per SIMD (a 7-wave cap measured within 1 %)
 // XCD-aware tile order.  Workgroup L of a 1-D launch runs on XCD L mod 8 (the
 // dispatcher deals workgroups round-robin over the 8 XCDs, each with its own
 // L2), so consecutive tiles of the row-major order would sit on different
@@ -110,7 +105,7 @@ inline FlowTiles flow_tiles(int64_t nx, int strips) {
 inline unsigned flow_blocks(const FlowTiles& ft) { return 8u * (unsigned)ft.per_xcd; }
 
 template <class R, bool DMAX>
-__global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
+__global__ __launch_bounds__(kFlowTX, kFlowWaves) void k_ice_flow(const FlowGrid g, const FlowK K, double* __restrict__ out,
                                                       int strip0, int strip_step, double* __restrict__ out_ice,
                                                       const FlowTiles ft) {
 #pragma clang fp contract(off)
@@ -237,19 +232,9 @@ __global__ __launch_bounds__(kFlowTX, TFG_FLOW_WAVES) void k_ice_flow(const Flow
       ow[q] = ow[q + 1];
     }
   };
-#if TFG_FLOW_PF2
-  Raw buf0, buf1;  // two rows in flight: rows of even / odd offset
-  if (r0 + 2 <= r1) fetch(r0 + 2, buf0);
-  if (r0 + 3 <= r1) fetch(r0 + 3, buf1);
-  for (int64_t r = r0; r < r1; r += 2) {
-    row(r, buf0, 4);
-    if (r + 1 < r1) row(r + 1, buf1, 4);
-  }
-#else
-  Raw buf;
+  Raw buf;  // one row in flight (two, with 5 waves per SIMD, measured 3 % slower: HISTORY.md section 6)
   if (r0 + 2 <= r1) fetch(r0 + 2, buf);
   for (int64_t r = r0; r < r1; ++r) row(r, buf, 3);
-#endif
   if constexpr (DMAX) {
     red[t] = dmax;
     __syncthreads();

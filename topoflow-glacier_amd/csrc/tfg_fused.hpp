@@ -24,19 +24,9 @@ using tfg::CellStatic;
 using tfg::CellStaticF;
 using tfg::DevParams;
 
-#ifndef TFG_BLOCK
-#define TFG_BLOCK 256
-#endif
-constexpr int kBlock = TFG_BLOCK;  // threads per workgroup
-#ifndef TFG_CELLS_PER_THREAD
-#define TFG_CELLS_PER_THREAD 1
-#endif
-constexpr int kCellsPerThread = TFG_CELLS_PER_THREAD;  // adjacent cells per lane
-#ifndef TFG_PREFETCH_DEPTH
-#define TFG_PREFETCH_DEPTH 2  // time steps of forcing requested ahead by the fast engine (1, 2; 3 to measure)
-#endif
-constexpr int kPrefetchFast = TFG_PREFETCH_DEPTH;
-static_assert(kPrefetchFast >= 1 && kPrefetchFast <= 3, "TFG_PREFETCH_DEPTH is 1, 2 or 3");
+constexpr int kBlock = 256;          // threads per workgroup
+constexpr int kCellsPerThread = 1;   // cells per lane (the streamed step accesses are per cell)
+constexpr int kPrefetchFast = 2;     // time steps of forcing the fast engine requests ahead (HISTORY.md section 5)
 constexpr int kWaves = kBlock / 64;
 constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
 constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
@@ -71,31 +61,10 @@ struct KArgs {
 // for the whole launch, which spills them to VGPR lanes and reads each back
 // with a v_readlane (a VALU instruction) at every use.
 static_assert(offsetof(KArgs, p) == 0, "KArgs::p is read at the start of the kernel-argument segment");
-#ifndef TFG_PARAM_RELOAD
-#define TFG_PARAM_RELOAD 1  // k_fused and k_cell_run re-read the model constants every step
-#endif
-#if TFG_PARAM_RELOAD
 #define TFG_STEP_PARAMS(p)                                                                                  \
   auto p##_ks = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr(); \
   asm volatile("" : "+s"(p##_ks));                                                                          \
   const DevParams& p = *(const DevParams*)p##_ks
-#else
-#define TFG_STEP_PARAMS(p) const DevParams& p = a.p
-#endif
-
-// The constants re-read at each phase of the fp64 step (TFG_EXACT_PHASES):
-// each call re-defines the kernel-argument pointer, so a phase's scalar loads
-// cannot be hoisted into an earlier phase.
-#ifndef TFG_EXACT_PHASES
-#define TFG_EXACT_PHASES 0
-#endif
-struct KernargParams {
-  __device__ const DevParams& operator()() const {
-    auto k = (const __attribute__((address_space(4))) DevParams*)__builtin_amdgcn_kernarg_segment_ptr();
-    asm volatile("" : "+s"(k));
-    return *(const DevParams*)k;
-  }
-};
 
 // Vector load/store of C adjacent cells (C*sizeof(T) <= 16 B per lane).
 template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
@@ -104,16 +73,11 @@ template <class T, int C> struct alignas(C * sizeof(T)) Pack { T v[C]; };
 // offset): the global_load/store "saddr" form, one offset VGPR per element
 // size instead of a 64-bit address per field (tfg_create keeps n_pad*8 < 2^32).
 //
-// TFG_LANE_OFF: re-materialise the 32-bit lane offset at each use (empty asm),
-// so instruction selection, which works per basic block, sees base + zext(off)
+// lane_off re-materialises the 32-bit lane offset at each use (empty asm), so
+// instruction selection, which works per basic block, sees base + zext(off)
 // and picks the saddr form instead of a per-lane 64-bit add.
-#ifndef TFG_LANE_OFF
-#define TFG_LANE_OFF 1
-#endif
 __device__ __forceinline__ uint32_t lane_off(uint32_t off) {
-#if TFG_LANE_OFF
   asm volatile("" : "+v"(off));
-#endif
   return off;
 }
 template <class T, int C>
@@ -133,33 +97,17 @@ __device__ __forceinline__ void vstore(T* __restrict__ base, uint32_t i, const T
 }
 // Streamed accesses of the step loop: forcing frames and window slots are read
 // once per step and history outputs written once, with far more traffic than
-// the caches hold before any reuse.  TFG_NT_LOAD / TFG_NT_STORE select the
-// non-temporal forms for them (A/B switch).
-#ifndef TFG_NT_LOAD
-#define TFG_NT_LOAD 0
-#endif
-#ifndef TFG_NT_STORE
-#define TFG_NT_STORE 1
-#endif
-// `off` is the lane's byte offset, materialised once per basic block by the
-// caller (lane_off), shared by every access of that block.
+// the caches hold before any reuse.  Stores are non-temporal; non-temporal
+// loads measured no better (HISTORY.md section 5).  `off` is the lane's byte
+// offset, materialised once per basic block by the caller (lane_off), shared
+// by every access of that block.
 template <class T>
 __device__ __forceinline__ T sload(const T* __restrict__ base, uint32_t off) {
-  const T* p = reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
-#if TFG_NT_LOAD
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
+  return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + off);
 }
 template <class T>
 __device__ __forceinline__ void sstore(T* __restrict__ base, uint32_t off, T v) {
-  T* p = reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
-#if TFG_NT_STORE
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
+  __builtin_nontemporal_store(v, reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off));
 }
 template <int C> __device__ __forceinline__ void dload(const double* p, uint32_t i, double (&v)[C]) { vload<double, C>(p, i, v); }
 template <int C> __device__ __forceinline__ void dstore(double* p, uint32_t i, const double (&v)[C]) { vstore<double, C>(p, i, v); }
@@ -203,32 +151,17 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
   }
 }
 
-#ifndef TFG_WG_PERM
-#define TFG_WG_PERM 0
-#endif
-#ifndef TFG_STEP_SKEW
-#define TFG_STEP_SKEW 1  // k_fused steps the plane stride, skew cells included (0: only the cells;
-                         // same-box A/B neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, 0 at 4096^2,
-                         // profiles/r4d_ab_skew.json)
-#endif
 #ifdef TFG_WG_TIMING  // diagnostic builds (tests/diagnostics/wg_timeline.py): for the first
                       // TFG_WG_TIMING workgroups of every k_fused launch, the wall clock
                       // (100 MHz) at start and end and the XCC / CU it ran on
 static __device__ unsigned long long g_wg_times[TFG_WG_TIMING][3];
 #endif
-#ifndef TFG_START_STAGGER
-#define TFG_START_STAGGER 0
-#endif
-#ifndef TFG_MIN_WAVES
-#define TFG_MIN_WAVES 4  // __launch_bounds__ minimum waves per SIMD (occupancy hint)
-#endif
-#ifndef TFG_MIN_WAVES_EXACT
-#define TFG_MIN_WAVES_EXACT 2  // fp64 engine: 256 VGPRs, no scratch spills
-#endif
+constexpr int kMinWaves = 4;       // __launch_bounds__ minimum waves per SIMD: fp32 engine, <= 128 VGPRs
+constexpr int kMinWavesExact = 2;  // fp64 engine: 256 VGPRs, no scratch spills
 // NS (fast engine only): the NaN-safe form of the step (tfg::cell_step_fast),
 // for launches the host could not verify to read only finite values.
 template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false>
-__global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+__global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : kMinWaves) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
                                                   const float* __restrict__ geo,   // [kGeoF][n_pad] f32 + [2][n_pad] f64
@@ -248,30 +181,16 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
   for (int i = threadIdx.x; i < kWaves * nb; i += kBlock) lds_bins[i] = ((i % 6) == 5) ? -INFINITY : 0.0;
   __syncthreads();
   double* wbins = lds_bins + (threadIdx.x >> 6) * nb;
-#if TFG_START_STAGGER  // measurement switch: the first round of resident workgroups starts at staggered
-                       // times, 0 .. TFG_START_STAGGER-1 sleeps of ~3.4 us, spread over every XCD
-  if (blockIdx.x < 1024) {
-    const int d = (int)((blockIdx.x >> 3) % TFG_START_STAGGER);
-    for (int i = 0; i < d; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-#endif
 
   const int64_t n_pad = a.n_pad;
-#if TFG_STEP_SKEW  // the whole plane stride, the skew's padding cells included
+  // the whole plane stride, the skew's padding cells included (stepping only the cells
+  // measured neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, profiles/r4d_ab_skew.json)
   const int64_t ngroups = n_pad / C;
-#else             // the cells rounded up to a wave
-  const int64_t ngroups = ((a.n + 63) & ~(int64_t)63) / C;
-#endif
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
   const int64_t nchunks = (ngroups + kBlock - 1) / kBlock;
-#if TFG_WG_PERM  // measurement switch: consecutive workgroups take chunks TFG_WG_PERM apart (a permutation
-                 // when gridDim is not a multiple of it), so the resident ones spread over the whole shard
-  const int64_t wg = ((int64_t)blockIdx.x * TFG_WG_PERM) % gridDim.x;
-#else
   const int64_t wg = blockIdx.x;
-#endif
   const int64_t g0 = (wg * nchunks / gridDim.x) * kBlock;
   const int64_t g1 = std::min<int64_t>(((wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
@@ -404,11 +323,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
             CellOut o;
             CellDiag& d = CATCH ? cacc[j] : acc;
             const bool valid = (c0 + j) < a.n;
-#if TFG_EXACT_PHASES
-            const KernargParams params;
-#else
             const tfg::ParamsAsIs params{p};
-#endif
             tfg::cell_step_exact<QC>(p, SX[j], u, (double)f.P[j], (double)f.T[j], (double)f.Q[j], (double)f.PA[j],
                                      (double)f.UZ[j], f.q[j], qn[j], cs[j], o, d, valid, (double)qc[j], params);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
@@ -434,7 +349,8 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
       };
       // The fast engine requests two steps ahead (three register sets, loop
       // unrolled by three, 127 VGPRs): +1.2-2.6 % at 1024^2, 2048^2 and 8192^2
-      // in same-box A/Bs against one step ahead (HISTORY.md section 5).  Step
+      // in same-box A/Bs against one step ahead, and three steps ahead measured
+      // no better (HISTORY.md section 5).  Step
       // k + 2's window slot is then read before steps k and k + 1 write theirs,
       // so a fused launch needs ring_len > 2 (launch_steps runs shorter windows
       // one step per launch).  The conduction (QC) and NaN-safe (NS) forms keep
@@ -449,20 +365,6 @@ __global__ __launch_bounds__(kBlock, EXACT ? TFG_MIN_WAVES_EXACT : TFG_MIN_WAVES
           fetch(k + 1, fb);
           advance(k, fa);
           fa = fb;
-        }
-      } else if constexpr (kAhead == 3) {  // measurement variant (TFG_PREFETCH_DEPTH=3)
-        Frame fc, fd;
-        fetch(1, fb);
-        fetch(2, fc);
-        for (int k = 0; k < a.K; k += 4) {
-          fetch(k + 3, fd);
-          advance(k, fa);
-          fetch(k + 4, fa);
-          if (k + 1 < a.K) advance(k + 1, fb);
-          fetch(k + 5, fb);
-          if (k + 2 < a.K) advance(k + 2, fc);
-          fetch(k + 6, fc);
-          if (k + 3 < a.K) advance(k + 3, fd);
         }
       } else if constexpr (kAhead == 2) {
         Frame fc;

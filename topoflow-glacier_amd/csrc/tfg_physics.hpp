@@ -80,6 +80,16 @@ struct DevParams {
   float f_qfac;               // dt*ws*2^36: snowfall-window slot scale
   float f_dt, f_T0;
   float f_c_eccs;             // rho_snow*Cp_snow*dt*ws                       :1527-1533
+  // scaled logarithm arguments (v_log_f32's -0.44 ulp bias is of its RESULT, so
+  // arguments scaled by a power of two to ~1 keep it off the energy terms)
+  float f_inv_z0s;            // 2^-k / z0: roughness log log2((z - h)/z0) = log2((z - h) f_inv_z0s) + k   :670
+  float f_l2k, f_l2k2, f_l2kk;  // k, 2k, k^2
+  float f_l2min;              // 0.01 * 2^-k: the clamp of :670 on the scaled argument
+  float f_em_sc;              // 0.1 * 2^10: em_air's (e/T)^(1/7) = (e f_em_sc / T)^(1/7) 2^(-10/7)  :1167
+  float f_ccFs;               // f_ccF * 2^(-10/7)
+  float f_Fm1;                // F - 1: em_air - 1 for the long-wave balance
+  float f_eps100_lo, f_ome100_lo;  // 100 eps - f_eps100, 100 (1 - eps) - f_ome100
+  float f_c6_hi, f_c6_lo;     // 1/6.1121 as hi + lo                          :888
 };
 
 // Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
@@ -1012,6 +1022,9 @@ __device__ __forceinline__ double root7_d(double x) {
 #ifndef TFG_LW_SPLIT
 #define TFG_LW_SPLIT 0  // 1: the fp32 long-wave balance without its cancellation (below)
 #endif
+#ifndef TFG_R5
+#define TFG_R5 0
+#endif
 
 template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
@@ -1058,22 +1071,43 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
                                    root7_d((e_d * 0.1) * rcp_d((double)T_air + 273.15)), p.F);
 #endif
 #else
+#if TFG_R5 & 8
+  // e_air = Hum P_air / (eps100 + ome100 Hum) as e0 + el (the products' and
+  // the quotient's rounding errors carried), then ln(e_air / 6.1121) by one
+  // Newton step from v_log_f32 whose residual is formed from e0 + el exactly
+  const float ph = Hum_sp * P_air, pl = fmaf(Hum_sp, P_air, -ph);
+  const float dh = fmaf(p.f_ome100, Hum_sp, p.f_eps100);
+  const float dl = fmaf(p.f_ome100, Hum_sp, p.f_eps100 - dh) + fmaf(p.f_ome100_lo, Hum_sp, p.f_eps100_lo);
+  float rd = frcp(dh);
+  rd = fmaf(fmaf(-dh, rd, 1.0f), rd, rd);
+  const float e_air = ph * rd;
+  const float el = (fmaf(-e_air, dh, ph) + fmaf(-e_air, dl, pl)) * rd;
+  const float ah = e_air * p.f_c6_hi, al = fmaf(e_air, p.f_c6_hi, -ah);  // e0 / 6.1121 = ah + al
+  const float ly = flog2(ah);
+  const float Ey = fexp2(-ly);
+  const float lr = fmaf(fmaf(e_air, p.f_c6_lo, fmaf(el, p.f_c6_hi, al)), Ey, fmaf(ah, Ey, -1.0f));
+  const float log_term = fmaf(ly, kLn2, lr);
+#elif TFG_R5 & 4
+  float rd = frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
+  rd = fmaf(fmaf(-(p.f_eps100 + p.f_ome100 * Hum_sp), rd, 1.0f), rd, rd);
+  const float e_air = Hum_sp * P_air * rd;
+  const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
+#else
   const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
   // dew point (:888-893) and surface temperature (:906-910)
   // ln(e_air / 6.1121) as the log of the ratio (~1): v_log_f32's mean error is
   // -0.44 ulp of its result, so a result near zero keeps that bias negligible,
   // where log2(e_air) - log2(6.1121) would carry it into T_dew
-#ifndef TFG_DEW_RATIO
-#define TFG_DEW_RATIO 1
-#endif
-#if TFG_DEW_RATIO && TFG_LOG_NEWTON >= 1
   const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
-#elif TFG_DEW_RATIO
-  const float log_term = flog2(e_air * (1.0f / 6.1121f)) * kLn2;
-#else
-  const float log_term = flog2(e_air) * kLn2 - 1.8102704f;
 #endif
+#if TFG_R5 & 4
+  const float dden = 18.678f - log_term;
+  float rdd = frcp(dden);
+  rdd = fmaf(fmaf(-dden, rdd, 1.0f), rdd, rdd);
+  const float T_dew = 257.14f * log_term * rdd;
+#else
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
+#endif
   const float T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
 #endif
   const float RH = e_air * inv_esat;
@@ -1100,10 +1134,33 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
 #else
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
+#if TFG_R5 & 16
+  float rb = frcp(bot);
+  rb = fmaf(fmaf(-bot, rb, 1.0f), rb, rb);
+  const float Ri = p.f_gz * dTs * rb;
+#else
   const float Ri = p.f_gz * dTs * frcp(bot);
+#endif
+#if TFG_R5 & 1
+  // log2((z - h_snow)/z0) = ly + k with ly = log2((z - h_snow) 2^-k / z0) ~ 0: squared as ly (ly + 2k) + k^2
+  const float ly2 = flog2(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0s, p.f_l2min));
+  const float L2sq = fmaf(ly2, ly2 + p.f_l2k2, p.f_l2kk);
+#else
   const float L2 = flog2_split(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
-  const float Dn = uz * p.f_k2 * frcp(L2 * L2);
+  const float L2sq = L2 * L2;
+#endif
+#if TFG_R5 & 16
+  float rl = frcp(L2sq);
+  rl = fmaf(fmaf(-L2sq, rl, 1.0f), rl, rl);
+  const float Dn = uz * p.f_k2 * rl;
+  const float d10 = fmaf(10.0f, Ri, 1.0f);
+  float rh = frcp(d10);
+  rh = fmaf(fmaf(-d10, rh, 1.0f), rh, rh);
+  const float Dh = (Ri > 0.0f) ? Dn * rh : Dn * fmaf(-10.0f, Ri, 1.0f);
+#else
+  const float Dn = uz * p.f_k2 * frcp(L2sq);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
+#endif
 #endif
   // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
   // (:853), written without the cancellation of the two near-equal pressures:
@@ -1185,10 +1242,27 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float Qn_SW = K_cs * (1.0f - albedo);
   // longwave (:1167-1248)
   float em_air;
+#if TFG_R5 & 2
+  float em_m1;  // em_air - 1, for the long-wave balance
+#endif
   if (!p.satterlund) {
+#if TFG_R5 & 1
+    const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));  // argument ~1: no log bias
+    em_air = fmaf(p.f_ccFs, em_r, p.f_F);
+#if TFG_R5 & 2
+    em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);
+#endif
+#else
     em_air = fmaf(p.f_ccF, fexp2(flog2_split(e_air * 0.1f * rT) * (1.0f / 7.0f)), p.f_F);
+#if TFG_R5 & 2
+    em_m1 = em_air - 1.0f;
+#endif
+#endif
   } else {
     em_air = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
+#if TFG_R5 & 2
+    em_m1 = em_air - 1.0f;
+#endif
   }
 #if TFG_ACC_EM
   // (e/T)^(1/7) from fp64 e_air and T_K, rounded to fp32 once (:1167)
@@ -1206,7 +1280,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const double a2 = TK_d2 * TK_d2, s2 = tks * tks;
   const double Qn_LW_d = p.em_surf_sigma * fma(em_d, a2 * a2, -(s2 * s2));
   const float Qn_LW = (float)Qn_LW_d;
-#elif TFG_LW_SPLIT
+#elif TFG_LW_SPLIT || (TFG_R5 & 2)
   // em Ta^4 - Ts^4 without its cancellation (LW_in ~ LW_out ~ 300 W m-2 net
   // ~100): (em - 1) Ta^4 + (Ta - Ts)(Ta + Ts)(Ta^2 + Ts^2), with Ta - Ts the
   // degC difference dTs (exact of the two fp32 sums' rounding) and em - 1 exact;
@@ -1215,7 +1289,11 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K;
   const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
+#if TFG_R5 & 2
+  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
+#else
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air - 1.0f, ta2 * ta2, d4);
+#endif
   const double Qn_LW_d = (double)Qn_LW;
 #else
   const float T_surf_K = T_surf + 273.15f;

@@ -310,6 +310,11 @@ class GlacierEngine:
         self._chk(self.lib.tfg_nan_safe_launches(self.h, ctypes.byref(c)))
         return int(c.value)
 
+    def set_step_form(self, nan_safe: bool) -> None:
+        """Run every launch of the fp32 engine in its NaN-safe step form
+        (True), or let each launch choose (False, the default; tfg_set_step_form)."""
+        self._chk(self.lib.tfg_set_step_form(self.h, 1 if nan_safe else 0))
+
     def set_stream(self, stream_ptr: int | None) -> None:
         self._chk(self.lib.tfg_set_stream(self.h, ctypes.c_void_p(stream_ptr or 0)))
         self._stream_ptr = stream_ptr or None
