@@ -10,19 +10,48 @@ floored error, the kind of step it sits on:
              gates diverged; harness.melt_out_flips (b))
   onset      SM starts (reference SM 0 at the step before, > 0 now)
   ordinary   anything else
-  python tests/diagnostics/tail_classify.py DUMP.npz [DUMP.npz ...] [--thr 7e-6]
+  python tests/diagnostics/tail_classify.py DUMP.npz [DUMP.npz ...] [--thr 7e-6] [--reclassify]
+With --reclassify the dump's cells are classified again by the current
+tests/harness.py rules (the dump's own `ok` mask is from the rules of the run
+that wrote it), with the whole-sample floors the dump kept.
 Diagnostic only.
 """
 import sys
 
+from pathlib import Path
+
 import numpy as np
 
+ROOT = Path(__file__).resolve().parents[2]
 NAMES = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
 
 
-def classify(z, thr):
+def reclassify(z):
+    """The compare mask of the dump's cells under the current harness rules."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "oracle"), str(ROOT / "topoflow-glacier_amd")]
+    import bench
+    import tests.harness as H
+
     fl = dict(zip([str(x) for x in z["names"]], z["floors"]))
-    ok = z["ok"]
+    G = {v: np.ascontiguousarray(z["gpu_" + v], dtype=np.float64) for v in NAMES}
+    R = {v: np.ascontiguousarray(z["ref_" + v], dtype=np.float64) for v in NAMES}
+    C = {v: np.ascontiguousarray(z["c64_" + v], dtype=np.float64) for v in NAMES}
+    for t in ("Qn_SW", "Qn_LW", "Qh", "Qe"):
+        R[t] = z["ref_" + t]
+    ids = {id(R[v]): fl[v] for v in NAMES}
+    orig = H.scale_floor
+    H.scale_floor = lambda a: ids[id(a)] if id(a) in ids else orig(a)  # the whole sample's floors
+    try:
+        dt = 0.25 if "--dt 0.25" in str(z["args"]) else 1.0
+        cls = H.classify_sample(G, R, C, dict(bench.BASE_CFG, dt=dt), 1e-5, True)
+    finally:
+        H.scale_floor = orig
+    return cls.ok, len(cls.genuine)
+
+
+def classify(z, thr, ok=None):
+    fl = dict(zip([str(x) for x in z["names"]], z["floors"]))
+    ok = z["ok"] if ok is None else ok
     G = {v: z["gpu_" + v] for v in NAMES}
     R = {v: z["ref_" + v] for v in NAMES}
     nsteps, ncell = R["SM"].shape
@@ -55,12 +84,14 @@ def main():
     thr = float(sys.argv[sys.argv.index("--thr") + 1]) if "--thr" in sys.argv else 7e-6
     for f in files:
         z = np.load(f)
-        rows = classify(z, thr)
+        ok, ngen = reclassify(z) if "--reclassify" in sys.argv else (None, None)
+        rows = classify(z, thr, ok)
         kinds = {}
         for r in rows:
             kinds.setdefault(r[4], []).append(r[0])
         print(f"{f}: {z['args']}  flips {int(z['n_flips'])}/{int(z['n_flips64'])} excused {int(z['n_excused'])} "
-              f"onsets {int(z['n_onsets'])}  max {z['worst'][0]:.4e}  fp64 baseline max {float(z['c64_max_floored']):.4e}")
+              f"onsets {int(z['n_onsets'])}  max {z['worst'][0]:.4e}  fp64 baseline max {float(z['c64_max_floored']):.4e}"
+              + (f"  reclassified: max {rows[0][0] if rows else 0.0:.4e} genuine {ngen}" if ok is not None else ""))
         for kind, es in sorted(kinds.items()):
             print(f"   {kind:9s} entries > {thr:.0e}: {len(es):4d}   max {max(es):.4e}")
         for e, v, c, k, kind in rows[:8]:

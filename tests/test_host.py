@@ -255,7 +255,12 @@ def test_bmi_grid_topology_of_the_raster():
     assert m.get_grid_node_count(0) == 12 and m.get_grid_size(0) == 12
     np.testing.assert_array_equal(m.get_grid_x(0, np.zeros(nx)), [0, 500, 1000, 1500])
     np.testing.assert_array_equal(m.get_grid_y(0, np.zeros(ny)), [1000, 500, 0])  # row 0 = north
-    np.testing.assert_array_equal(m.get_grid_origin(0, np.zeros(2)), [0, 0])  # the south-west node
+    # uniform_rectilinear: node (k, j) at origin + (k, j) * spacing, the origin the north-west node, dy < 0
+    org, sp = m.get_grid_origin(0, np.zeros(2)), m.get_grid_spacing(0, np.zeros(2))
+    np.testing.assert_array_equal(org, [1000, 0])
+    np.testing.assert_array_equal(sp, [-500, 500])
+    np.testing.assert_array_equal(org[0] + np.arange(ny) * sp[0], m.get_grid_y(0, np.zeros(ny)))
+    np.testing.assert_array_equal(org[1] + np.arange(nx) * sp[1], m.get_grid_x(0, np.zeros(nx)))
     with pytest.raises(NotImplementedError):
         m.get_grid_z(0, np.zeros(1))
     ne, nf = m.get_grid_edge_count(0), m.get_grid_face_count(0)
@@ -275,7 +280,7 @@ def test_bmi_grid_topology_of_the_raster():
         a, b = fn[:, k], fn[:, (k + 1) % 4]
         assert all(sorted(en[e]) == sorted((i, j)) for e, i, j in zip(fe[:, k], a, b))
     m.cfg = SimpleNamespace(da=0.25, dx=30.0, dy=40.0)  # the lateral terms' spacing when configured
-    np.testing.assert_array_equal(m.get_grid_spacing(0, np.zeros(2)), [40.0, 30.0])
+    np.testing.assert_array_equal(m.get_grid_spacing(0, np.zeros(2)), [-40.0, 30.0])
     np.testing.assert_array_equal(m.get_grid_x(0, np.zeros(nx)), [0, 30, 60, 90])
 
 

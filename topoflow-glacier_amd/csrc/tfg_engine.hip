@@ -568,14 +568,13 @@ enum : uint8_t { kUnknown = 0, kOk = 1, kDirty = 2 };
 // its exp / log / constant-divisor division (tfg_fastmath.hpp) on device, with
 // the device libm's exp and log beside them
 __global__ void k_selftest_powers(const double* __restrict__ x, double* __restrict__ y, int64_t n, int which) {
-  const double inv7 = 1.0 / 7.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double v = x[i];
     double r;
     switch (which) {
       case 0: r = tfg::pow4(v); break;
       case 1: r = tfg::pow1p5(v); break;
-      case 2: r = tfg::pow_small_root(v, inv7); break;
+      case 2: r = tfg::root7(v); break;
       case 3: r = tfg_fm::exp_k(v); break;
       case 4: r = exp(v); break;
       case 5: r = tfg_fm::log_k(v); break;

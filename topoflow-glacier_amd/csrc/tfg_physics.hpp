@@ -22,6 +22,10 @@
 
 #include "tfg_fastmath.hpp"
 
+#ifndef TFG_R5
+#define TFG_R5 0
+#endif
+
 namespace tfg {
 
 using tfg_fm::div_k;
@@ -364,15 +368,55 @@ __device__ __forceinline__ double pow1p5(double x) {
 #pragma clang fp contract(off)
   return x * __builtin_sqrt(x);
 }
-// em_air's (e/T)^(1/7) (:1167) as exp(log(x)/7): x is ~2e-3, so the log's
-// rounding moves the exponent by ~1e-16 and the result stays within ~3 ulp of
-// numpy's pow, while the general pow's extra-precision log and special cases
-// cost about twice the log + exp pair.  The one-cell step batches the log with
-// level 1's logs and the exp with level 2's exps, which leaves no general pow
-// in its chain unless SATTERLUND is set.
-__device__ __forceinline__ double pow_small_root(double x, double inv_n) {
+// em_air's (e/T)^(1/7) (:1167): an fp32 seed exp2(log2(x)/7) (relative error
+// ~2e-7) and two Newton steps y <- (6 y + x / y^6) / 7 (error 3 e^2 each, so
+// ~1e-13 then rounding), the reciprocal from v_rcp_f64 and two Newton steps:
+// within 2 ulp of numpy's x ** (1/7) (tests/test_power_rewrites.py), at about
+// half the cost of a log and an exp (round 5; before: exp(log(x)/7)).  x = 0
+// gives 0, a negative or NaN x NaN and +inf +inf, as numpy's power.
+__device__ __forceinline__ double rcp_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+  return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+}
+__device__ __forceinline__ double root7(double x) {
 #pragma clang fp contract(off)
-  return exp_ks(log_k(x) * inv_n);
+  const double y0 = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf((float)x) * (1.0f / 7.0f));
+  double y = y0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const double y2 = y * y;
+    const double y6 = (y2 * y2) * y2;
+    y = __builtin_fma(y, 6.0 / 7.0, (x * rcp_nr(y6)) * (1.0 / 7.0));
+  }
+  return (x > 0.0 && x < INFINITY) ? y : y0;
+}
+
+// Stull's wet bulb (:1514-1520, RH a fraction), fp64, with two arctangents for
+// four (round 5; ~1e-15 from the reference's form, tests/test_gpu_parity.py):
+//   atan(T + RH) - atan(RH - 1.676331) = atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))
+//       (+ pi sign(T + RH) where the denominator is negative), and
+//   atan(0.023101 RH) by its series to x^9 (relative error x^10/11 < 1e-9 below
+//       RH = 8, on a term below 1e-3 K; lanes above take atan).
+// wet_bulb_parts gives the two arctangent arguments; wet_bulb_finish the rest
+// from their arctangents (the one-cell step batches the arctangents).
+constexpr double kPi = 3.141592653589793;
+__device__ __forceinline__ void wet_bulb_parts(double T_air, double RH, double& u0, double& u1, double& den) {
+#pragma clang fp contract(off)
+  u0 = 0.151977 * sqrt(RH + 8.313659);
+  den = 1.0 + (T_air + RH) * (RH - 1.676331);
+  u1 = (T_air + 1.676331) / den;
+}
+__device__ __forceinline__ double atan_small_series(double x) {
+#pragma clang fp contract(off)
+  const double x2 = x * x;
+  return x * (1.0 + x2 * (-1.0 / 3.0 + x2 * (1.0 / 5.0 + x2 * (-1.0 / 7.0 + x2 * (1.0 / 9.0)))));
+}
+__device__ __forceinline__ double wet_bulb_finish(double T_air, double RH, double at0, double at1, double den,
+                                                   double at_small) {
+#pragma clang fp contract(off)
+  const double d = den < 0.0 ? at1 + copysign(kPi, T_air + RH) : at1;
+  return T_air * at0 + d + ((0.00391838 * pow1p5(RH)) * at_small) - 4.86035;
 }
 
 // ---------------------------------------------------------------------------
@@ -478,7 +522,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * pow_small_root(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K, p3.one_seventh);
+    const double term1 = p3.one_minus_F_172 * root7(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K);
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
     em_air = 1.08 * (1.0 - exp_ks(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
@@ -494,8 +538,12 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // Stull wet bulb (:1514-1520), only needed where it snows
   double T_wb = 0.0;
   if (P_snow > 0.0) {
-    T_wb = T_air * atan(0.151977 * sqrt(RH + 8.313659)) + atan(T_air + RH) - atan(RH - 1.676331) +
-           ((0.00391838 * pow1p5(RH)) * atan(0.023101 * RH)) - 4.86035;
+    double u0, u1, den;
+    wet_bulb_parts(T_air, RH, u0, u1, den);
+    const double x = 0.023101 * RH;
+    double at_small = atan_small_series(x);
+    if (__any(RH > 8.0)) at_small = RH > 8.0 ? atan(x) : at_small;
+    T_wb = wet_bulb_finish(T_air, RH, atan(u0), atan(u1), den, at_small);
   }
   const DevParams& p4 = params();  // melt and mass phase
   melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
@@ -584,9 +632,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const double x_alb = -st.n * r_alb;                          // :1041
     ex1 = exp_k(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
-  if (X.mine(X_LOG1))  // :670, :888, and em_air's root (:1167, pow_small_root)
-    lg1 = log_k(lane == 1 ? npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01)
-                          : (lane == 2 ? div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K : div_k(e_air, 6.1121, 1.0 / 6.1121)));
+  if (X.mine(X_LOG1))  // :670, :888
+    lg1 = log_k(lane == 1 ? npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01) : div_k(e_air, 6.1121, 1.0 / 6.1121));
   if (X.mine(X_TRIG1)) ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325 (one argument)
   cos_wl = cos_hour_angle(s, u);                                                          // SF:867
   if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
@@ -597,7 +644,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   X.put(X_POW1, pw1);
   if (W > 1) lds_level_barrier();
   const double e_p0 = X.get(X_EXP1, ex1, 0), e_es = X.get(X_EXP1, ex1, 1), e_alb = X.get(X_EXP1, ex1, 2);
-  const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1), log_em = X.get(X_LOG1, lg1, 2);
+  const double log_term = X.get(X_LOG1, lg1, 0), log_dn = X.get(X_LOG1, lg1, 1);
   const double pw_em = X.get(X_POW1, pw1, 0), pw_es = X.get(X_POW1, pw1, 2);
   const double pw_ta4 = pow4(T_air_K);  // :1231
   if (W > 1) ac = X.get(X_TRIG1, 0.0, 0);
@@ -639,13 +686,14 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (X.mine(X_EXP2)) {
     double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
     if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
-    if (lane == 3) ea2 = log_em * p.one_seventh;                                    // :1167 (pow_small_root)
     ex2 = exp_k(ea2);
   }
   if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15));  // :796 (surface)
-  if (X.mine(X_ATAN2) && P_snow > 0.0)  // Stull wet bulb (:1514-1520), only where it snows
-    at2 = atan(lane == 1 ? T_air + RH : (lane == 2 ? RH - 1.676331 : (lane == 3 ? 0.023101 * RH
-                                                                                 : 0.151977 * sqrt(RH + 8.313659))));
+  // Stull wet bulb (:1514-1520), only where it snows: wet_bulb_parts' two arguments and, for RH > 8,
+  // the small term's own arctangent
+  double wb_u0 = 0.0, wb_u1 = 0.0, wb_den = 1.0;
+  if (P_snow > 0.0) wet_bulb_parts(T_air, RH, wb_u0, wb_u1, wb_den);
+  if (X.mine(X_ATAN2) && P_snow > 0.0) at2 = atan(lane == 1 ? wb_u1 : (lane == 2 ? 0.023101 * RH : wb_u0));
   X.put(X_EXP2, ex2);
   X.put(X_POW2, pw2);
   X.put(X_ATAN2, at2);
@@ -679,7 +727,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :1167-1192, :1231-1248
   double em_air;
   if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * X.get(X_EXP2, ex2, 3);
+    const double term1 = p.one_minus_F_172 * root7(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K);
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
@@ -692,8 +740,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + qc;
   double T_wb = 0.0;
   if (P_snow > 0.0) {
-    T_wb = T_air * X.get(X_ATAN2, at2, 0) + X.get(X_ATAN2, at2, 1) - X.get(X_ATAN2, at2, 2) +
-           ((0.00391838 * pow1p5(RH)) * X.get(X_ATAN2, at2, 3)) - 4.86035;
+    const double at_small = RH > 8.0 ? X.get(X_ATAN2, at2, 2) : atan_small_series(0.023101 * RH);
+    T_wb = wet_bulb_finish(T_air, RH, X.get(X_ATAN2, at2, 0), X.get(X_ATAN2, at2, 1), wb_den, at_small);
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
@@ -847,16 +895,37 @@ __device__ __forceinline__ double add_rounded(double h, double a, double b) {
   return h + a * b;
 }
 
+// Stull's wet-bulb temperature (:1514-1520) of the air temperature [degC] and
+// RH as a fraction (the reference's quirk), fp32.  Two rewrites keep it cheap
+// (every wave with a snowing lane evaluates it: 99 % of the bench's wave-steps
+// for 12 % of its cell-steps):
+//   atan(T + RH) - atan(RH - 1.676331) = atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))
+//       (+ pi sign(T + RH) when the denominator is negative): one arctangent for two;
+//   0.00391838 RH^1.5 atan(0.023101 RH), a term below 1e-3 K for RH < 5, with
+//       atan(x) = x (1 - x^2/3 + x^4/5) (relative error x^6/7 < 3e-7 below RH = 8;
+//       waves with a lane above that take fast_atanf).
+__device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
+#if TFG_R5 & 32
+  const float a = T_air + rh, b = rh - 1.676331f;
+  const float den = fmaf(a, b, 1.0f);
+  float d = fast_atanf((T_air + 1.676331f) * frcp(den));
+  if (den < 0.0f) d += copysignf(3.14159265358979f, a);
+  const float x = 0.023101f * rh, x2 = x * x;
+  float at = x * fmaf(fmaf(0.2f, x2, -0.333333333f), x2, 1.0f);
+  if (__any(rh > 8.0f)) at = rh > 8.0f ? fast_atanf(x) : at;
+  return T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + d +
+         (0.00391838f * (rh * __builtin_sqrtf(rh))) * at - 4.86035f;
+#else
+  return T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
+         fast_atanf(rh - 1.676331f) + (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) -
+         4.86035f;
+#endif
+}
+
 // Cold content a snowfall brings (:1507-1537): rho_s Cp_s (P_snow dt ws)
-// (T0 - T_wb), with Stull's wet-bulb temperature of RH as a fraction (the
-// reference's quirk), fp32: melt_core's increment, for the diagnostic build
-// (melt_core keeps its own copy of the expression, which compiles to the
-// instruction sequence the PMC profiles were measured on).
+// (T0 - T_wb), fp32 (melt_core's increment, for the diagnostic build).
 __device__ __forceinline__ float snowfall_cold(const DevParams& p, float P_snow, float rh, float T_air) {
-  const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
-                     fast_atanf(rh - 1.676331f) +
-                     (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
-  return p.f_c_eccs * P_snow * (p.f_T0 - T_wb);
+  return p.f_c_eccs * P_snow * (p.f_T0 - wet_bulb_f(rh, T_air));
 }
 
 // Per-cell partial sums of the fast variant over one launch's steps (fp32;
@@ -908,15 +977,8 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P
   const double SM = ts * (1.0 / 3600.0);
   h_swe = dmax<NS>(sub_rounded(h_swe, SM, p.dt3600), 0.0);  // dt*3600 folded: exact for dt = 2^k
   // snowfall cold content (:1507-1537), Stull wet bulb with RH as a fraction
-  // (snowfall_cold spells out the same increment for the diagnostic build)
   double Eccs = Eccs0;
-  if (P_snow > 0.0f) {
-    const float rh = RH;
-    const float T_wb = T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
-                       fast_atanf(rh - 1.676331f) +
-                       (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) - 4.86035f;
-    Eccs = dmax<NS>(Eccs + (double)(p.f_c_eccs * P_snow * (p.f_T0 - T_wb)) - E_in, 0.0);
-  }
+  if (P_snow > 0.0f) Eccs = dmax<NS>(Eccs + (double)snowfall_cold(p, P_snow, RH, T_air) - E_in, 0.0);
   // ice melt (:1418-1434), cap (:1473-1480), integral (:1493), update_iwe (:1612-1617)
   const double E_rem_i = dmax<NS>(E_in - Ecci0, 0.0);
   double IM = (h_swe == 0.0 && previous_swe == 0.0) ? E_rem_i * p.inv_dt_rhoLf : 0.0;
@@ -1022,9 +1084,7 @@ __device__ __forceinline__ double root7_d(double x) {
 #ifndef TFG_LW_SPLIT
 #define TFG_LW_SPLIT 0  // 1: the fp32 long-wave balance without its cancellation (below)
 #endif
-#ifndef TFG_R5
-#define TFG_R5 0
-#endif
+
 
 template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
@@ -1092,6 +1152,14 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   rd = fmaf(fmaf(-(p.f_eps100 + p.f_ome100 * Hum_sp), rd, 1.0f), rd, rd);
   const float e_air = Hum_sp * P_air * rd;
   const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
+#elif TFG_R5 & 64
+  const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
+  // ln(e_air / 6.1121) with 1/6.1121 as hi + lo and the product's rounding
+  // carried into the Newton residual (no constant or rounding bias)
+  const float ah = e_air * p.f_c6_hi, al = fmaf(e_air, p.f_c6_hi, -ah) + e_air * p.f_c6_lo;
+  const float ly = flog2(ah);
+  const float Ey = fexp2(-ly);
+  const float log_term = fmaf(ly, kLn2, fmaf(al, Ey, fmaf(ah, Ey, -1.0f)));
 #else
   const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
   // dew point (:888-893) and surface temperature (:906-910)
@@ -1105,6 +1173,10 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   float rdd = frcp(dden);
   rdd = fmaf(fmaf(-dden, rdd, 1.0f), rdd, rdd);
   const float T_dew = 257.14f * log_term * rdd;
+#elif TFG_R5 & 64
+  // 257.14 and 18.678 as hi + lo: their fp32 roundings (+5.7e-8, -2.7e-8) were a T_dew bias of ~1e-6 K
+  const float T_dew = fmaf(log_term, 257.14f, log_term * -1.4648438e-05f) *
+                      frcp((18.678f - log_term) + 5.0354004e-07f);
 #else
   const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
 #endif
@@ -1289,7 +1361,14 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K;
   const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
-#if TFG_R5 & 2
+#if (TFG_R5 & 2) && (TFG_R5 & 128)
+  // Ta^4 with Ta = T_air + 273.15 exactly: the fp32 sum's rounding and 273.15f's
+  // (-6.1e-6 K) as lo, Ta^4 = ta^4 (1 + 4 lo / ta): a +-1.5e-5 K error of Ta
+  // was +-2.2e-7 of (em - 1) Ta^4 ~ 75 W m-2
+  const float tlo = ((273.15f - T_K) + T_air) + 6.1035156e-06f;
+  const float t1 = em_m1 * (ta2 * ta2);
+  const float Qn_LW = p.f_em_surf_sigma * (fmaf(t1, 4.0f * tlo * rT, t1) + d4);
+#elif TFG_R5 & 2
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
 #else
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air - 1.0f, ta2 * ta2, d4);

@@ -596,18 +596,27 @@ class BmiTopoflowGlacier(BmiBase):
         return shape
 
     def get_grid_spacing(self, grid: int, spacing):
-        # (dy, dx) [m] in shape order: the configured spacing of the lateral
-        # terms when given, otherwise square cells of area `da` [km2]
-        dx, dy = getattr(self.cfg, "dx", None), getattr(self.cfg, "dy", None)
-        if dx is not None and dy is not None:
-            spacing[:] = (float(dy), float(dx))
-        else:
-            d = float(np.sqrt(self.cfg.da) * 1000.0)
-            spacing[:] = (d, d)
+        # (dy, dx) [m] in shape order, dy NEGATIVE: row 0 is the northern edge,
+        # so y falls by |dy| per row from the origin (get_grid_origin, the
+        # north-west node), and origin + index * spacing gives every node's
+        # coordinates, as get_grid_x / get_grid_y report them.  |dx|, |dy|: the
+        # configured spacing of the lateral terms when given, otherwise square
+        # cells of area `da` [km2].  (Additive: the reference leaves the grid
+        # functions unimplemented.)
+        dx, dy = self._cell_size()
+        spacing[:] = (-dy, dx)
         return spacing
 
+    def _cell_size(self) -> tuple[float, float]:
+        dx, dy = getattr(self.cfg, "dx", None), getattr(self.cfg, "dy", None)
+        if dx is not None and dy is not None:
+            return float(dx), float(dy)
+        d = float(np.sqrt(self.cfg.da) * 1000.0)
+        return d, d
+
     def get_grid_origin(self, grid: int, origin):
-        origin[:] = (0.0, 0.0)
+        # (y, x) of node 0 (row 0, column 0): the north-west corner node
+        origin[:] = ((self.ny - 1) * self._cell_size()[1], 0.0)
         return origin
 
     def get_grid_type(self, grid: int) -> str:
@@ -619,16 +628,16 @@ class BmiTopoflowGlacier(BmiBase):
     # by row (index = row * nx + col, the layout of every value array), and
     # row 0 is the NORTHERN edge, as in the engine: tfg_terrain_from_dem and
     # the conduction and ice-flow halos pair halo_north with row 0.  So y
-    # decreases with the row index: row k sits at y = (ny - 1 - k) * dy above
-    # the origin (get_grid_origin), the lower-left (south-west) node.  Edges
+    # decreases with the row index: row k sits at y = (ny - 1 - k) * |dy|
+    # above the south-west node, i.e. at origin + k * spacing with the origin
+    # the north-west node and a negative dy (get_grid_origin, get_grid_spacing).  Edges
     # are the nx - 1 x-edges of each row, then the nx y-edges of each row
     # pair; faces are the cells between four nodes, counter-clockwise in
     # (x, y) from the lower-left node, with edges in the same order.
     def _axis(self, k: int) -> np.ndarray:
         sp = self.get_grid_spacing(0, np.empty(2))
-        n = (self.ny, self.nx)[k]
-        a = np.arange(n, dtype=np.float64) * sp[k]
-        return a[::-1].copy() if k == 0 else a
+        o = self.get_grid_origin(0, np.empty(2))
+        return o[k] + np.arange((self.ny, self.nx)[k], dtype=np.float64) * sp[k]
 
     def get_grid_x(self, grid: int, x):
         x[:] = self._axis(1)
