@@ -12,6 +12,8 @@ extern "C" void fm_eval(const double* x, double* y, long n, int which) {
       case 5: y[i] = tfg_fm::log_k(v); break;
       case 7: y[i] = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
       case 8: y[i] = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
+      case 10: y[i] = tfg_fm::fdiv(v, 7.3); break;
+      case 11: y[i] = tfg_fm::fdiv(7.3, v); break;
       default: y[i] = 0.0; break;
     }
   }
@@ -20,4 +22,9 @@ extern "C" void fm_eval(const double* x, double* y, long n, int which) {
 // div_k(x[i], c[i], RN(1/c[i])) for arbitrary divisors
 extern "C" void fm_div(const double* x, const double* c, double* y, long n) {
   for (long i = 0; i < n; ++i) y[i] = tfg_fm::div_k(x[i], c[i], 1.0 / c[i]);
+}
+
+// fdiv(x[i], c[i]): the variable-divisor quotient
+extern "C" void fm_fdiv(const double* x, const double* c, double* y, long n) {
+  for (long i = 0; i < n; ++i) y[i] = tfg_fm::fdiv(x[i], c[i]);
 }

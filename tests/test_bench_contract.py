@@ -177,6 +177,9 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     # the drop-in legs: per-step K = 1 launches from device inputs, and queued steps; defer_update instances
     g = d["dropin_per_step_grid"]
     assert g["per_step"]["value"] > 0 and g["queued"]["value"] > 0 and g["per_step"]["bytes_per_cell_update"] == 184
+    # the same-run A/B of the step forms at K = 1: device-set inputs run NaN-safe, host-checked frames clean
+    assert g["per_step"]["nan_safe_launches"] == 24 and g["clean_form_step_launch"]["nan_safe_launches"] == 0
+    assert g["clean_form_step_launch"]["nan_safe_over_clean"] > 0
     mi = d["dropin_defer_update_instances"]
     assert mi["instances"] == 64 and mi["us_per_instance_step"] > 0 and mi["all_instances_equal"]
     ts = rf["traffic_source"]  # no PMC profile of this shape: traffic is null and says why

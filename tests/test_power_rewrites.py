@@ -58,6 +58,36 @@ def test_seventh_root_by_newton():
     assert edge[0] == 0.0 and np.isnan(edge[1]) and edge[2] == np.inf
 
 
+# The Stull wet bulb's atan(0.151977 sqrt(RH + 8.313659)) on RH in [0, 5] as
+# the engines evaluate it (csrc/tfg_physics.hpp stull_atan0_poly, wet_bulb_f):
+# Horner in t = 0.4 RH - 1 with the coefficients restated here.
+STULL64 = [float.fromhex(h) for h in (
+    "0x1.da94c1a0c29f5p-2", "0x1.7aac28df5f664p-5", "-0x1.ea2542f0a20c4p-9", "0x1.bc9c3023533e3p-12",
+    "-0x1.f1959460701e0p-15", "0x1.3be2008d543e9p-17", "-0x1.b16bbee999fe5p-20", "0x1.38df9b2403c64p-22",
+    "-0x1.d44af1ebe2f10p-25", "0x1.686a49a337c49p-27", "-0x1.17d5b0c2a427ap-29", "0x1.acccbc15e0e7fp-32",
+    "-0x1.a2f6161678e01p-34", "0x1.b58d687bb4412p-36")]
+STULL32 = [0.4634580910205841, 0.046224694699048996, -0.003739525331184268, 0.0004237863759044558,
+           -5.9253852668916807e-05, 9.90594708127901e-06, -1.7216859760083025e-06]
+
+
+def test_stull_arctangent_fits():
+    """The fp64 fit is within 2e-14 and the fp32 one within 1.2e-7 (the fp32
+    engine's atan is good to 1.5e-7) of arctan(0.151977 sqrt(RH + 8.313659))
+    over [0, 5], the range the engines use them on (other RH take atan)."""
+    rh = np.linspace(0.0, 5.0, 200_001)
+    ref = np.arctan(0.151977 * np.sqrt(rh + 8.313659))
+    t = 0.4 * rh - 1.0
+    y = np.full_like(t, STULL64[-1])
+    for c in STULL64[-2::-1]:
+        y = y * t + c
+    assert (np.abs(y - ref) / ref).max() <= 2e-14
+    t32 = np.float32(0.4) * rh.astype(np.float32) - np.float32(1.0)
+    y32 = np.full_like(t32, np.float32(STULL32[-1]))
+    for c in STULL32[-2::-1]:
+        y32 = (y32 * t32 + np.float32(c)).astype(np.float32)
+    assert (np.abs(y32.astype(np.float64) - ref) / ref).max() <= 1.2e-7
+
+
 def _device(x, which):
     """The engine's own device functions (tfg_selftest_powers: pow4, pow1p5,
     root7 of csrc/tfg_physics.hpp) on x."""

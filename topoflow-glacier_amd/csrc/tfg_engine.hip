@@ -581,6 +581,8 @@ __global__ void k_selftest_powers(const double* __restrict__ x, double* __restri
       case 6: r = log(v); break;
       case 7: r = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
       case 9: r = tfg_fm::exp_ks(v); break;
+      case 10: r = tfg_fm::fdiv(v, 7.3); break;
+      case 11: r = tfg_fm::fdiv(7.3, v); break;
       default: r = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
     }
     y[i] = r;
@@ -874,6 +876,8 @@ void derive_params(const tfg_params& q, DevParams& p) {
   }
   p.f_em_sc = 102.4f;  // 0.1 * 2^10
   p.f_ccFs = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0));
+  p.f_ccFs_lo = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0) - (double)p.f_ccFs);
+  p.f_esig_lo = (float)(p.em_surf_sigma - (double)p.f_em_surf_sigma);
   p.f_Fm1 = (float)(q.canopy_factor - 1.0);
   p.f_eps100_lo = (float)(100.0 * q.eps - (double)p.f_eps100);
   p.f_ome100_lo = (float)(100.0 * (1.0 - q.eps) - (double)p.f_ome100);
@@ -1604,7 +1608,7 @@ int tfg_reset_diag(tfg_handle* h) {
 }
 
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out) {
-  if (!x || !out || n < 0 || which < 0 || which > 9) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  if (!x || !out || n < 0 || which < 0 || which > 11) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
   if (n == 0) return TFG_OK;
   HIPCHK(nullptr, hipSetDevice(device));
   double* d = nullptr;

@@ -29,6 +29,7 @@
 namespace tfg {
 
 using tfg_fm::div_k;
+using tfg_fm::fdiv;
 using tfg_fm::exp_k;
 using tfg_fm::exp_ks;
 using tfg_fm::log_k;
@@ -90,7 +91,8 @@ struct DevParams {
   float f_l2k, f_l2k2, f_l2kk;  // k, 2k, k^2
   float f_l2min;              // 0.01 * 2^-k: the clamp of :670 on the scaled argument
   float f_em_sc;              // 0.1 * 2^10: em_air's (e/T)^(1/7) = (e f_em_sc / T)^(1/7) 2^(-10/7)  :1167
-  float f_ccFs;               // f_ccF * 2^(-10/7)
+  float f_ccFs, f_ccFs_lo;    // f_ccF * 2^(-10/7) as hi + lo
+  float f_esig_lo;            // em_surf*sigma - f_em_surf_sigma
   float f_Fm1;                // F - 1: em_air - 1 for the long-wave balance
   float f_eps100_lo, f_ome100_lo;  // 100 eps - f_eps100, 100 (1 - eps) - f_ome100
   float f_c6_hi, f_c6_lo;     // 1/6.1121 as hi + lo                          :888
@@ -392,12 +394,14 @@ __device__ __forceinline__ double root7(double x) {
   return (x > 0.0 && x < INFINITY) ? y : y0;
 }
 
-// Stull's wet bulb (:1514-1520, RH a fraction), fp64, with two arctangents for
-// four (round 5; ~1e-15 from the reference's form, tests/test_gpu_parity.py):
+// Stull's wet bulb (:1514-1520, RH a fraction), fp64, with one arctangent for
+// four (round 5; ~1e-14 from the reference's form, tests/test_gpu_parity.py):
 //   atan(T + RH) - atan(RH - 1.676331) = atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))
-//       (+ pi sign(T + RH) where the denominator is negative), and
-//   atan(0.023101 RH) by its series to x^9 (relative error x^10/11 < 1e-9 below
-//       RH = 8, on a term below 1e-3 K; lanes above take atan).
+//       (+ pi sign(T + RH) where the denominator is negative),
+//   atan(0.151977 sqrt(RH + 8.313659)) by stull_atan0_poly, and
+//   atan(0.023101 RH) by its series to x^9 (relative error x^10/11 < 1e-10 for
+//       RH <= 5, on a term below 1e-3 K);
+// waves with a lane whose RH is outside [0, 5] take the arctangents there.
 // wet_bulb_parts gives the two arctangent arguments; wet_bulb_finish the rest
 // from their arctangents (the one-cell step batches the arctangents).
 constexpr double kPi = 3.141592653589793;
@@ -405,8 +409,30 @@ __device__ __forceinline__ void wet_bulb_parts(double T_air, double RH, double& 
 #pragma clang fp contract(off)
   u0 = 0.151977 * sqrt(RH + 8.313659);
   den = 1.0 + (T_air + RH) * (RH - 1.676331);
-  u1 = (T_air + 1.676331) / den;
+  u1 = fdiv(T_air + 1.676331, den);
 }
+// atan(0.151977 sqrt(RH + 8.313659)) for RH in [0, 5] as a degree-13
+// polynomial in t = 0.4 RH - 1 (a Chebyshev fit, relative error < 2e-14,
+// tests/test_power_rewrites.py): 13 FMAs for a square root and an arctangent.
+__device__ __forceinline__ double stull_atan0_poly(double RH) {
+  const double t = __builtin_fma(0.4, RH, -1.0);
+  double y = 0x1.b58d687bb4412p-36;
+  y = __builtin_fma(y, t, -0x1.a2f6161678e01p-34);
+  y = __builtin_fma(y, t, 0x1.acccbc15e0e7fp-32);
+  y = __builtin_fma(y, t, -0x1.17d5b0c2a427ap-29);
+  y = __builtin_fma(y, t, 0x1.686a49a337c49p-27);
+  y = __builtin_fma(y, t, -0x1.d44af1ebe2f10p-25);
+  y = __builtin_fma(y, t, 0x1.38df9b2403c64p-22);
+  y = __builtin_fma(y, t, -0x1.b16bbee999fe5p-20);
+  y = __builtin_fma(y, t, 0x1.3be2008d543e9p-17);
+  y = __builtin_fma(y, t, -0x1.f1959460701e0p-15);
+  y = __builtin_fma(y, t, 0x1.bc9c3023533e3p-12);
+  y = __builtin_fma(y, t, -0x1.ea2542f0a20c4p-9);
+  y = __builtin_fma(y, t, 0x1.7aac28df5f664p-5);
+  return __builtin_fma(y, t, 0x1.da94c1a0c29f5p-2);
+}
+// RH outside the fits' range [0, 5] (NaN stays on the fits and gives NaN)
+__device__ __forceinline__ bool stull_off_fit(double RH) { return (RH < 0.0) || (RH > 5.0); }
 __device__ __forceinline__ double atan_small_series(double x) {
 #pragma clang fp contract(off)
   const double x2 = x * x;
@@ -442,7 +468,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
   // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556
   const double T_K = T_air + 273.15;
-  double p0 = p.sea_p0 * exp_k(p.negM_g * s.elev / (p.R * T_K));
+  double p0 = p.sea_p0 * exp_k(fdiv(p.negM_g * s.elev, p.R * T_K));
   p0 = div_k(p0, 1000.0, 1.0 / 1000.0);
   p0 = p0 * 10.0;
   // :567, :576, :585, :604, :613, :623
@@ -457,37 +483,37 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // saturation vapour pressure (air) :788-802
   double e_sat_air;
   if (!p.satterlund) {
-    e_sat_air = 0.611 * exp_ks((17.3 * T_air) / (T_air + 237.3));
+    e_sat_air = 0.611 * exp_ks(fdiv(17.3 * T_air, T_air + 237.3));
   } else {
-    e_sat_air = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_air + 273.15)), 1000.0, 1.0 / 1000.0);
+    e_sat_air = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1000.0, 1.0 / 1000.0);
   }
   e_sat_air = e_sat_air * 10.0;
   // :817-826
-  double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
+  double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
   e = div_k(e, 1000.0, 1.0 / 1000.0);
   const double e_air = e * 10.0;
-  const double RH = e_air / e_sat_air;  // :838
+  const double RH = fdiv(e_air, e_sat_air);  // :838
   // :888-893
   const double log_term = log_k(div_k(e_air, 6.1121, 1.0 / 6.1121));
-  const double T_dew = 257.14 * log_term / (18.678 - log_term);
+  const double T_dew = fdiv(257.14 * log_term, 18.678 - log_term);
   // :906-910 (previous-step depths)
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
   double e_sat_surf;
   if (!p.satterlund) {
-    e_sat_surf = 0.611 * exp_ks((17.3 * T_surf) / (T_surf + 237.3));
+    e_sat_surf = 0.611 * exp_ks(fdiv(17.3 * T_surf, T_surf + 237.3));
   } else {
-    e_sat_surf = div_k(pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
+    e_sat_surf = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
   }
   e_sat_surf = e_sat_surf * 10.0;
   // :640-644, per cell
   const double top = p.gz * (T_air - T_surf);
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
-  const double Ri = top / bot;
+  const double Ri = fdiv(top, bot);
   // :670-726
-  const double arg = p.kappa / log_k(npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01));
+  const double arg = fdiv(p.kappa, log_k(npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01)));
   const double Dn = uz * (arg * arg);
-  const double Dh = (Ri > 0.0) ? Dn / (1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
   // :744-745
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
   // :919-920
@@ -495,7 +521,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // :853 (SURFACE uses the air RH)
   const double e_surf = RH * e_sat_surf;
   // :931-934
-  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * fdiv(p.lhc, p0);
   // albedo :1023-1059 with the fixed-point window
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
   st.tot_q += window_tot(q_new) - window_tot(q_old);
@@ -522,7 +548,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * root7(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K);
+    const double term1 = p3.one_minus_F_172 * root7(fdiv(div_k(e_air, 10.0, 1.0 / 10.0), T_air_K));
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
     em_air = 1.08 * (1.0 - exp_ks(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
@@ -541,9 +567,13 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     double u0, u1, den;
     wet_bulb_parts(T_air, RH, u0, u1, den);
     const double x = 0.023101 * RH;
-    double at_small = atan_small_series(x);
-    if (__any(RH > 8.0)) at_small = RH > 8.0 ? atan(x) : at_small;
-    T_wb = wet_bulb_finish(T_air, RH, atan(u0), atan(u1), den, at_small);
+    double at0 = stull_atan0_poly(RH), at_small = atan_small_series(x);
+    if (__any(stull_off_fit(RH))) {
+      const bool off = stull_off_fit(RH);
+      at0 = off ? atan(u0) : at0;
+      at_small = off ? atan(x) : at_small;
+    }
+    T_wb = wet_bulb_finish(T_air, RH, at0, atan(u1), den, at_small);
   }
   const DevParams& p4 = params();  // melt and mass phase
   melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
@@ -614,7 +644,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   d.PR += P_rain * p.da_m2 * dt;
   d.PS += P_snow * p.da_m2 * dt;
   // :817-826
-  double e = Hum_sp * P_air / (p.eps + (p.one_minus_eps * Hum_sp));
+  double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
   e = div_k(e, 1000.0, 1.0 / 1000.0);
   const double e_air = e * 10.0;
   const double T_air_K = T_air + 273.15;
@@ -627,8 +657,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // ---- level 1: arguments from inputs, state, statics and uniforms
   double ex1 = 0.0, lg1 = 0.0, cos_wl = 0.0, ac = 0.0, pw1 = 0.0;
   if (X.mine(X_EXP1)) {
-    const double x_p0 = p.negM_g * s.elev / (p.R * T_K);        // :551
-    const double x_es = (17.3 * T_air) / (T_air + 237.3);        // :788
+    const double x_p0 = fdiv(p.negM_g * s.elev, p.R * T_K);       // :551
+    const double x_es = fdiv(17.3 * T_air, T_air + 237.3);        // :788
     const double x_alb = -st.n * r_alb;                          // :1041
     ex1 = exp_k(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
@@ -637,7 +667,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (X.mine(X_TRIG1)) ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325 (one argument)
   cos_wl = cos_hour_angle(s, u);                                                          // SF:867
   if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
-    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - 2353.0 / (T_air + 273.15) : div_k(T_air_K, 2016.0, 1.0 / 2016.0));
+    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - fdiv(2353.0, T_air + 273.15) : div_k(T_air_K, 2016.0, 1.0 / 2016.0));
   X.put(X_EXP1, ex1);
   X.put(X_LOG1, lg1);
   X.put(X_TRIG1, ac);
@@ -656,18 +686,18 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :788-802, :838
   double e_sat_air = !p.satterlund ? 0.611 * e_es : div_k(pw_es, 1000.0, 1.0 / 1000.0);
   e_sat_air = e_sat_air * 10.0;
-  const double RH = e_air / e_sat_air;
+  const double RH = fdiv(e_air, e_sat_air);
   // :888-893, :906-910
-  const double T_dew = 257.14 * log_term / (18.678 - log_term);
+  const double T_dew = fdiv(257.14 * log_term, 18.678 - log_term);
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
   // :640-644, :670-726, :744-745
   const double top = p.gz * (T_air - T_surf);
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
-  const double Ri = top / bot;
-  const double arg = p.kappa / log_dn;
+  const double Ri = fdiv(top, bot);
+  const double arg = fdiv(p.kappa, log_dn);
   const double Dn = uz * (arg * arg);
-  const double Dh = (Ri > 0.0) ? Dn / (1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
   // albedo (:1041-1059)
   const double snow_albedo = 0.4 + 0.44 * e_alb;
@@ -684,11 +714,11 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // ---- level 2: after T_dew, T_surf and RH
   double ex2 = 0.0, pw2 = 0.0, at2 = 0.0;
   if (X.mine(X_EXP2)) {
-    double ea2 = lane == 1 ? 0.0614 * T_dew : (17.3 * T_surf) / (T_surf + 237.3);  // :919, :788 (surface)
+    double ea2 = lane == 1 ? 0.0614 * T_dew : fdiv(17.3 * T_surf, T_surf + 237.3);  // :919, :788 (surface)
     if (p.satterlund && lane == 2) ea2 = -1.0 * pw_em;                             // :1190
     ex2 = exp_k(ea2);
   }
-  if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - 2353.0 / (T_surf + 273.15));  // :796 (surface)
+  if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15));  // :796 (surface)
   // Stull wet bulb (:1514-1520), only where it snows: wet_bulb_parts' two arguments and, for RH > 8,
   // the small term's own arctangent
   double wb_u0 = 0.0, wb_u1 = 0.0, wb_den = 1.0;
@@ -703,7 +733,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
   const double e_surf = RH * e_sat_surf;
-  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * (p.lhc / p0);
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * fdiv(p.lhc, p0);
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
   const double a_s = -0.0363 - (0.0084 * W_p);
@@ -727,7 +757,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :1167-1192, :1231-1248
   double em_air;
   if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * root7(div_k(e_air, 10.0, 1.0 / 10.0) / T_air_K);
+    const double term1 = p.one_minus_F_172 * root7(fdiv(div_k(e_air, 10.0, 1.0 / 10.0), T_air_K));
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
@@ -740,8 +770,10 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double Q_sum = Qn_SW + Qn_LW + Qh + Qe + 0.0 + qc;
   double T_wb = 0.0;
   if (P_snow > 0.0) {
-    const double at_small = RH > 8.0 ? X.get(X_ATAN2, at2, 2) : atan_small_series(0.023101 * RH);
-    T_wb = wet_bulb_finish(T_air, RH, X.get(X_ATAN2, at2, 0), X.get(X_ATAN2, at2, 1), wb_den, at_small);
+    const bool off = stull_off_fit(RH);
+    const double at0 = off ? X.get(X_ATAN2, at2, 0) : stull_atan0_poly(RH);
+    const double at_small = off ? X.get(X_ATAN2, at2, 2) : atan_small_series(0.023101 * RH);
+    T_wb = wet_bulb_finish(T_air, RH, at0, X.get(X_ATAN2, at2, 1), wb_den, at_small);
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
@@ -912,9 +944,17 @@ __device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
   if (den < 0.0f) d += copysignf(3.14159265358979f, a);
   const float x = 0.023101f * rh, x2 = x * x;
   float at = x * fmaf(fmaf(0.2f, x2, -0.333333333f), x2, 1.0f);
-  if (__any(rh > 8.0f)) at = rh > 8.0f ? fast_atanf(x) : at;
-  return T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + d +
-         (0.00391838f * (rh * __builtin_sqrtf(rh))) * at - 4.86035f;
+  // atan(0.151977 sqrt(rh + 8.313659)) on [0, 5]: degree-6 fit in t = 0.4 rh - 1 (relative error < 1e-7)
+  const float t = fmaf(0.4f, rh, -1.0f);
+  float a0 = fmaf(fmaf(fmaf(fmaf(fmaf(fmaf(-1.7216859760083025e-06f, t, 9.90594708127901e-06f), t,
+                                       -5.9253852668916807e-05f), t, 0.0004237863759044558f), t,
+                             -0.003739525331184268f), t, 0.046224694699048996f), t, 0.4634580910205841f);
+  if (__any((rh < 0.0f) || (rh > 5.0f))) {  // outside the fits (NaN stays on them)
+    const bool off = (rh < 0.0f) || (rh > 5.0f);
+    a0 = off ? fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) : a0;
+    at = off ? fast_atanf(x) : at;
+  }
+  return T_air * a0 + d + (0.00391838f * (rh * __builtin_sqrtf(rh))) * at - 4.86035f;
 #else
   return T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
          fast_atanf(rh - 1.676331f) + (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) -
@@ -1107,7 +1147,16 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   d.PS += P_snow;
   // vapour pressures [mbar] (:788-826); RH = e_air / e_sat_air (:838)
   // Brutsaert: e_sat = 6.11 exp(17.3 T/(T+237.3)); Satterlund: 10^(11.4-2353/T_K)/100
+#if TFG_R5 & 256
+  float rA = rT;
+  if (!p.satterlund) {
+    const float ta = T_air + 237.3f;
+    rA = frcp(ta);
+    rA = fmaf(fmaf(-ta, rA, 1.0f), rA, rA);
+  }
+#else
   const float rA = p.satterlund ? rT : frcp(T_air + 237.3f);
+#endif
   float inv_esat;
   if (!p.satterlund) {
     inv_esat = (1.0f / 6.11f) * fexp2((-17.3f * kLog2e) * T_air * rA);
@@ -1238,7 +1287,13 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // (:853), written without the cancellation of the two near-equal pressures:
   //   e_air - e_surf = -e_air*expm1(x),  x = -k*dTs/((T_s+c)(T_a+c))
   // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15)
+#if TFG_R5 & 256
+  const float tsc = T_surf + (p.satterlund ? 273.15f : 237.3f);
+  float rS = frcp(tsc);
+  rS = fmaf(fmaf(-tsc, rS, 1.0f), rS, rS);
+#else
   const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
+#endif
 #ifndef TFG_DE_EXPM1
 #define TFG_DE_EXPM1 0
 #endif
@@ -1321,7 +1376,9 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
 #if TFG_R5 & 1
     const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));  // argument ~1: no log bias
     em_air = fmaf(p.f_ccFs, em_r, p.f_F);
-#if TFG_R5 & 2
+#if (TFG_R5 & 2) && (TFG_R5 & 128)
+    em_m1 = fmaf(p.f_ccFs, em_r, fmaf(p.f_ccFs_lo, em_r, p.f_Fm1));
+#elif TFG_R5 & 2
     em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);
 #endif
 #else
@@ -1367,7 +1424,8 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // was +-2.2e-7 of (em - 1) Ta^4 ~ 75 W m-2
   const float tlo = ((273.15f - T_K) + T_air) + 6.1035156e-06f;
   const float t1 = em_m1 * (ta2 * ta2);
-  const float Qn_LW = p.f_em_surf_sigma * (fmaf(t1, 4.0f * tlo * rT, t1) + d4);
+  const float lw = fmaf(t1, 4.0f * tlo * rT, t1) + d4;
+  const float Qn_LW = fmaf(p.f_em_surf_sigma, lw, p.f_esig_lo * lw);
 #elif TFG_R5 & 2
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
 #else
