@@ -1,4 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 python -m pytest tests -q -m gpu ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1; echo "pytest rc=$?"
-tail -60 gpurun_out/gpu_tests.log
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} \
+  > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+echo "pytest rc=$rc"
+tail -40 gpurun_out/gpu_tests.log
+exit $rc

@@ -1,0 +1,54 @@
+"""The deepest launch the bench times, checked exactly as the bench checks it.
+
+At N = 4 the driver's strong-scaling line gives each rank a 2048 x 8192 shard
+of the 8192^2 grid (BASELINE config 4) and bench.auto_fuse a 384-step launch:
+the longest fp32 launch of any bench line, so the one where the flux error
+accumulates furthest.  This runs rank 0's parity check of that line on one GPU
+(bench.capture_parity: a one-step lead-in, then ONE 384-step launch over the
+whole shard; bench.sample_parity: the numpy oracle on the same cells, the
+classification of tests/harness.py) on global rows 0-9 -- a superset of the
+rows 0-7 the N = 4 line samples itself -- and holds its max_floored_rel to
+8e-6, the 1e-5 tolerance with a 20 % margin.
+"""
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MARGIN_TOL = 8e-6
+
+
+def test_n4_rank0_deep_launch_sample(monkeypatch):
+    import torch
+
+    import bench
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+    from topoflow_glacier.synthetic import diurnal_table
+
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--ny", "8192", "--nx", "8192", "--parity-cells", str(10 * 8192)])
+    args = bench.parse()
+    world, rank = 4, 0
+    plan = bench.shard_plan(args, world, rank)
+    assert (plan["row0"], plan["rows"]) == (0, 2048)
+    args.fuse = bench.auto_fuse(plan["rows"] * args.nx)
+    assert args.fuse == 384
+    cfg = TopoflowGlacierConfig.model_validate(dict(bench.BASE_CFG, ny=plan["rows"], nx=args.nx, dt=args.dt))
+    eng = GlacierEngine(cfg, plan["rows"], args.nx, engine="float32", device=0, n_frames=args.frames,
+                        hist_depth=args.fuse, fuse_steps=args.fuse)
+    try:
+        eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
+        cap = bench.capture_parity(eng, args, plan, world, torch, 0)
+    finally:
+        eng.close()
+    assert cap["plan"]["launch_steps"] == [1, 384] and cap["plan"]["rows"] == 10
+    par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
+    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
+                               "flips_fp64_baseline", "depletion_steps", "melt_onsets_explained")})
+    assert par["global_rows"] == [0, 9]
+    assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
+    assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
+    assert par["max_floored_rel_fp64_baseline"] < 1e-12
+    assert np.isfinite(par["max_floored_rel_incl_depletion_rates"])

@@ -852,14 +852,11 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.f_ome100 = (float)(100.0 * (1.0 - q.eps));
   p.f_gz = (float)p.gz;
   p.f_z = 10.0f;
-  p.f_inv_z0 = (float)(1.0 / q.z0_air);
   p.f_k2 = (float)((q.kappa / std::log(2.0)) * (q.kappa / std::log(2.0)));
   p.f_rho_air_Cp_air = (float)p.rho_air_Cp_air;
   p.f_qe = (float)(p.rho_air_Lv * q.latent_heat_constant * 100.0 / q.sea_level_p0);
   p.f_dust = (float)q.dust_atten;
   p.f_1pdust = (float)(1.0 + q.dust_atten);
-  p.f_ccF = (float)(p.one_minus_F_172 * p.cloud_term);
-  p.f_F = (float)q.canopy_factor;
   p.f_em_surf_sigma = (float)p.em_surf_sigma;
   p.f_qfac = (float)(q.dt * p.ws * p.qscale);
   p.f_dt = (float)q.dt;
@@ -869,20 +866,13 @@ void derive_params(const tfg_params& q, DevParams& p) {
   {
     const int k = (int)std::lround(std::log2(0.7 * p.z / q.z0_air));  // (z - h)/z0 near 2^k for h ~ 0.3 z
     p.f_inv_z0s = (float)std::ldexp(1.0 / q.z0_air, -k);
-    p.f_l2k = (float)k;
     p.f_l2k2 = (float)(2 * k);
     p.f_l2kk = (float)(k * k);
     p.f_l2min = (float)std::ldexp(0.01, -k);
   }
   p.f_em_sc = 102.4f;  // 0.1 * 2^10
   p.f_ccFs = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0));
-  p.f_ccFs_lo = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0) - (double)p.f_ccFs);
-  p.f_esig_lo = (float)(p.em_surf_sigma - (double)p.f_em_surf_sigma);
   p.f_Fm1 = (float)(q.canopy_factor - 1.0);
-  p.f_eps100_lo = (float)(100.0 * q.eps - (double)p.f_eps100);
-  p.f_ome100_lo = (float)(100.0 * (1.0 - q.eps) - (double)p.f_ome100);
-  p.f_c6_hi = (float)(1.0 / 6.1121);
-  p.f_c6_lo = (float)(1.0 / 6.1121 - (double)p.f_c6_hi);
 }
 
 void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {

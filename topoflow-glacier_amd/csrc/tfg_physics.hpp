@@ -22,10 +22,6 @@
 
 #include "tfg_fastmath.hpp"
 
-#ifndef TFG_R5
-#define TFG_R5 0
-#endif
-
 namespace tfg {
 
 using tfg_fm::div_k;
@@ -75,12 +71,11 @@ struct DevParams {
   // fast variant: fp32 constants, folded on the host in fp64
   float f_T_rs_dn;            // largest float <= T_rain_snow (exact T > T_rs test)
   float f_eps100, f_ome100;   // 100*eps, 100*(1-eps)                        :817-826
-  float f_gz, f_z, f_inv_z0;  // :640, :670
+  float f_gz, f_z;            // g*z, z                                       :640, :670
   float f_k2;                 // (kappa/ln 2)^2                               :670-672
   float f_rho_air_Cp_air;     // :744
   float f_qe;                 // rho_air*Lv*lhc*100/sea_p0: Qe = f_qe*Dh*de*exp(Mg elev/(R T))  :931-934, :551-556
   float f_dust, f_1pdust;     // dust_atten, 1 + dust_atten                  SF:610, SF:652
-  float f_ccF, f_F;           // (1-F)*1.72*(1+0.22C^2), F                    :1167-1175
   float f_em_surf_sigma;      // em_surf*sigma: Qn_LW = em_s*sigma*(em_air*Ta^4 - Ts^4)  :1231-1248
   float f_qfac;               // dt*ws*2^36: snowfall-window slot scale
   float f_dt, f_T0;
@@ -88,14 +83,11 @@ struct DevParams {
   // scaled logarithm arguments (v_log_f32's -0.44 ulp bias is of its RESULT, so
   // arguments scaled by a power of two to ~1 keep it off the energy terms)
   float f_inv_z0s;            // 2^-k / z0: roughness log log2((z - h)/z0) = log2((z - h) f_inv_z0s) + k   :670
-  float f_l2k, f_l2k2, f_l2kk;  // k, 2k, k^2
+  float f_l2k2, f_l2kk;       // 2k, k^2
   float f_l2min;              // 0.01 * 2^-k: the clamp of :670 on the scaled argument
   float f_em_sc;              // 0.1 * 2^10: em_air's (e/T)^(1/7) = (e f_em_sc / T)^(1/7) 2^(-10/7)  :1167
-  float f_ccFs, f_ccFs_lo;    // f_ccF * 2^(-10/7) as hi + lo
-  float f_esig_lo;            // em_surf*sigma - f_em_surf_sigma
+  float f_ccFs;               // (1-F)*1.72*(1+0.22C^2) * 2^(-10/7)            :1167-1175
   float f_Fm1;                // F - 1: em_air - 1 for the long-wave balance
-  float f_eps100_lo, f_ome100_lo;  // 100 eps - f_eps100, 100 (1 - eps) - f_ome100
-  float f_c6_hi, f_c6_lo;     // 1/6.1121 as hi + lo                          :888
 };
 
 // Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
@@ -803,25 +795,6 @@ struct CellStaticF {
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
-// log2 with the argument split as m * 2^e, m in [0.5, 1): v_log_f32 then only
-// sees m, whose result is in [-1, 0), so its mean error of -0.44 ulp of the
-// result stays ~1e-8 absolute instead of a relative bias on the whole log.
-// Used where the flux integrates into the state (energy bias accumulates).
-#ifndef TFG_SPLIT_LOG
-#define TFG_SPLIT_LOG 0
-#endif
-__device__ __forceinline__ float flog2_nr(float x);
-__device__ __forceinline__ float flog2_split(float x) {
-#if TFG_LOG_NEWTON >= 2
-  return flog2_nr(x);
-#elif TFG_SPLIT_LOG
-  const float m = __builtin_amdgcn_frexp_mantf(x);
-  const int e = __builtin_amdgcn_frexp_expf(x);
-  return (float)e + flog2(m);
-#else
-  return flog2(x);
-#endif
-}
 // log2 refined by one Newton step on exp2 (v_exp_f32 is unbiased; v_log_f32
 // has a mean error of -0.44 ulp of its result): y += (x*2^-y - 1)*log2(e).
 // The residual error is second order, so no bias reaches the state.
@@ -829,23 +802,14 @@ __device__ __forceinline__ float flog2_nr(float x) {
   const float y = flog2(x);
   return fmaf(fmaf(x, fexp2(-y), -1.0f), 1.4426950408889634f, y);
 }
-#ifndef TFG_LOG_NEWTON
-#define TFG_LOG_NEWTON 1  // 0: none, 1: dew point, 2: dew point, Dn and em_air
-#endif
-constexpr float kLog2e = 1.4426950408889634f;
-// expm1 without cancellation: Taylor polynomial (degree 8) for |x| < 0.5
-// (truncation < 1e-8 relative), exp2(x log2 e) - 1 beyond.
-__device__ __forceinline__ float fexpm1(float x) {
-  float q = 1.0f / 40320.0f;
-  q = fmaf(q, x, 1.0f / 5040.0f);
-  q = fmaf(q, x, 1.0f / 720.0f);
-  q = fmaf(q, x, 1.0f / 120.0f);
-  q = fmaf(q, x, 1.0f / 24.0f);
-  q = fmaf(q, x, 1.0f / 6.0f);
-  q = fmaf(q, x, 0.5f);
-  const float small = fmaf(q * x, x, x);
-  return fabsf(x) < 0.5f ? small : fexp2(x * kLog2e) - 1.0f;
+// 1/x: v_rcp_f32 (~1 ulp, biased) and one Newton step (correctly rounded but
+// for a rare last-bit miss, no bias): for the divisors whose quotient feeds
+// the dew point, which every flux term reads
+__device__ __forceinline__ float frcp_nr(float x) {
+  const float r = frcp(x);
+  return fmaf(fmaf(-x, r, 1.0f), r, r);
 }
+constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
 // fp64 derivation of the per-cell geometry (exact trig identities from
@@ -928,16 +892,16 @@ __device__ __forceinline__ double add_rounded(double h, double a, double b) {
 }
 
 // Stull's wet-bulb temperature (:1514-1520) of the air temperature [degC] and
-// RH as a fraction (the reference's quirk), fp32.  Two rewrites keep it cheap
+// RH as a fraction (the reference's quirk), fp32.  Three rewrites keep it cheap
 // (every wave with a snowing lane evaluates it: 99 % of the bench's wave-steps
 // for 12 % of its cell-steps):
 //   atan(T + RH) - atan(RH - 1.676331) = atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))
 //       (+ pi sign(T + RH) when the denominator is negative): one arctangent for two;
 //   0.00391838 RH^1.5 atan(0.023101 RH), a term below 1e-3 K for RH < 5, with
-//       atan(x) = x (1 - x^2/3 + x^4/5) (relative error x^6/7 < 3e-7 below RH = 8;
-//       waves with a lane above that take fast_atanf).
+//       atan(x) = x (1 - x^2/3 + x^4/5) (relative error x^6/7 < 3e-7 on [0, 5]);
+//   atan(0.151977 sqrt(RH + 8.313659)) as a polynomial fit on [0, 5].
+// Waves with a lane outside [0, 5] (or NaN) take fast_atanf for both.
 __device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
-#if TFG_R5 & 32
   const float a = T_air + rh, b = rh - 1.676331f;
   const float den = fmaf(a, b, 1.0f);
   float d = fast_atanf((T_air + 1.676331f) * frcp(den));
@@ -955,11 +919,6 @@ __device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
     at = off ? fast_atanf(x) : at;
   }
   return T_air * a0 + d + (0.00391838f * (rh * __builtin_sqrtf(rh))) * at - 4.86035f;
-#else
-  return T_air * fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) + fast_atanf(T_air + rh) -
-         fast_atanf(rh - 1.676331f) + (0.00391838f * (rh * __builtin_sqrtf(rh))) * fast_atanf(0.023101f * rh) -
-         4.86035f;
-#endif
 }
 
 // Cold content a snowfall brings (:1507-1537): rho_s Cp_s (P_snow dt ws)
@@ -999,15 +958,13 @@ struct MeltF {
   double h_swe, h_iwe, Eccs, Ecci;
   float SM, IM, Erem_s, IM_int;  // outputs; terms of the SM and IM integrals (:1486, :1493)
 };
-template <bool NS, class QS>
-__device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P_snow, float RH, float T_air,
+template <bool NS>
+__device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, float P_snow, float RH, float T_air,
                                            double h_swe0, double h_iwe0, double Eccs0, double Ecci0,
                                            double h_ice_prev) {
   MeltF m;
   const double previous_swe = h_swe0;
-  double E_in;
-  if constexpr (sizeof(QS) == 8) E_in = Q_sum * p.dt;  // an fp64 flux sum (TFG_QSUM_F64); dt in hours, as the reference (:1364)
-  else E_in = (double)(Q_sum * p.f_dt);
+  const double E_in = (double)(Q_sum * p.f_dt);  // dt in hours, as the reference (:1364)
   // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
   const double E_rem_s = dmax<NS>(E_in - Eccs0, 0.0);
   m.Erem_s = (float)E_rem_s;
@@ -1042,8 +999,8 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, QS Q_sum, float P
   m.IM = (float)IM;
   return m;
 }
-template <bool NS, class QS>
-__device__ __forceinline__ void melt_fast(const DevParams& p, QS Q_sum, float P_snow, float P_rain, float RH,
+template <bool NS>
+__device__ __forceinline__ void melt_fast(const DevParams& p, float Q_sum, float P_snow, float P_rain, float RH,
                                           float T_air, CellState& st, CellOutF& o, DiagF& d) {
   const MeltF m = melt_core<NS>(p, Q_sum, P_snow, RH, T_air, st.h_swe, st.h_iwe, st.Eccs, st.Ecci, st.h_ice);
   d.Erem_s += m.Erem_s;
@@ -1064,67 +1021,6 @@ __device__ __forceinline__ void melt_fast(const DevParams& p, QS Q_sum, float P_
   o.M_total = m.IM + m.SM + P_rain * (1.0f / 3600.0f);  // :1441-1443
   o.RH = RH;
 }
-
-// fp64 pieces for the fp32 engine's accuracy promotions (TFG_ACC, below).
-// rcp_d: 1/x from v_rcp_f32 and one fp64 Newton step (relative error ~1e-14;
-// x within fp32 range).  ln_d: ln x within 2e-11 for finite x > 0 (x = 2^e m,
-// m in [sqrt(1/2), sqrt(2)), ln m = 2 atanh((m-1)/(m+1)) as an odd series to
-// t^11, |t| <= 0.172; 100x below what the fp32 engine's tolerance needs of the
-// dew point and the roughness log), the hardware log for 0, inf and NaN (their
-// numpy values: -inf, inf, NaN).  root7_d: x^(1/7) from the fp32 power and one
-// Newton step (relative error ~1e-13).
-__device__ __forceinline__ double rcp_d(double x) {
-  const double r = (double)frcp((float)x);
-  return fma(r, fma(-x, r, 1.0), r);
-}
-__device__ __forceinline__ double ln_d(double x) {
-  int e = __builtin_amdgcn_frexp_exp(x);
-  double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1)
-  if (m < 0.70710678118654752) { m = m + m; e -= 1; }
-  const double t = (m - 1.0) * rcp_d(m + 1.0);
-  const double s = t * t;
-  double q = 1.0 / 11.0;
-  q = fma(q, s, 1.0 / 9.0);
-  q = fma(q, s, 1.0 / 7.0);
-  q = fma(q, s, 1.0 / 5.0);
-  q = fma(q, s, 1.0 / 3.0);
-  const double lm = fma(2.0 * t * s, q, 2.0 * t);
-  const double r = fma((double)e, 0.69314718055994531, lm);
-  return (x > 0.0 && x < INFINITY) ? r : (double)(flog2((float)x) * kLn2);
-}
-__device__ __forceinline__ double root7_d(double x) {
-  const double y = (double)fexp2(flog2((float)x) * (1.0f / 7.0f));
-  const double y2 = y * y;
-  const double y6 = y2 * y2 * y2;
-  const double r = fma(x * (1.0 / 7.0), rcp_d(y6), y * (6.0 / 7.0));
-  return (x > 0.0 && x < INFINITY) ? r : y;
-}
-
-// TFG_ACC: a bit mask of fp64 promotions of the fp32 engine's energy terms,
-// ordered by how much of its pure-relative error each removes
-// (tests/diagnostics/fp32_emulation.py, tests/diagnostics/term_attribution.py;
-// DESIGN.md section 3):
-//   1  LW    the long-wave balance (:1231-1248): T + 273.15, the fourth powers
-//            and their difference (LW_in ~ LW_out ~ 300 W m-2 cancel to ~100)
-//   2  DEW   e_air, the dew point, T_surf and T_air - T_surf (:809-911)
-//   4  EM    em_air's (e/T)^(1/7) (:1167)
-//   8  TURB  Ri, Dn, Dh and Qh (:626-745), the roughness log as fp32 + correction
-//  16  SUM   the flux sum and E_in (:1259-1319, :1364)
-#ifndef TFG_ACC
-#define TFG_ACC 0
-#endif
-#define TFG_ACC_LW ((TFG_ACC) & 1)
-#define TFG_ACC_DEW ((TFG_ACC) & 2)
-#define TFG_ACC_EM ((TFG_ACC) & 4)
-#define TFG_ACC_TURB ((TFG_ACC) & 8)
-#ifndef TFG_QSUM_F64
-#define TFG_QSUM_F64 0
-#endif
-#define TFG_ACC_SUM (((TFG_ACC) & 16) || TFG_QSUM_F64)
-#ifndef TFG_LW_SPLIT
-#define TFG_LW_SPLIT 0  // 1: the fp32 long-wave balance without its cancellation (below)
-#endif
-
 
 template <bool QC, bool NANSAFE>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
@@ -1147,170 +1043,43 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   d.PS += P_snow;
   // vapour pressures [mbar] (:788-826); RH = e_air / e_sat_air (:838)
   // Brutsaert: e_sat = 6.11 exp(17.3 T/(T+237.3)); Satterlund: 10^(11.4-2353/T_K)/100
-#if TFG_R5 & 256
-  float rA = rT;
-  if (!p.satterlund) {
-    const float ta = T_air + 237.3f;
-    rA = frcp(ta);
-    rA = fmaf(fmaf(-ta, rA, 1.0f), rA, rA);
-  }
-#else
   const float rA = p.satterlund ? rT : frcp(T_air + 237.3f);
-#endif
   float inv_esat;
   if (!p.satterlund) {
     inv_esat = (1.0f / 6.11f) * fexp2((-17.3f * kLog2e) * T_air * rA);
   } else {
     inv_esat = 100.0f * fexp2((2353.0f * rT - 11.4f) * 3.3219280948873626f);
   }
-#if TFG_ACC_DEW
-  // e_air [mbar] (:809-826), the dew point (:888-893) and the surface
-  // temperature (:906-910) in fp64
-  const double e_d = (double)Hum_sp * (double)P_air * rcp_d(fma(p.one_minus_eps, (double)Hum_sp, p.eps)) * 0.01;
-  const float e_air = (float)e_d;
-  const double L_d = ln_d(e_d * (1.0 / 6.1121));
-  const double T_dew_d = 257.14 * L_d * rcp_d(18.678 - L_d);
-  const double T_surf_d = (snow_pos || ice_pos) ? dmin<NS>(T_dew_d, 0.0) : T_dew_d;
-  // only the fp32-rounded results live on (register pressure): each is then
-  // within 6e-8 of its fp64 value, where the fp32 chain was ~1e-6 K off
-  const float T_dew = (float)T_dew_d, T_surf = (float)T_surf_d;
-  const float dTs = (float)((double)T_air - T_surf_d);
-#if TFG_ACC_EM
-  const float em_root = (float)fma(p.one_minus_F_172 * p.cloud_term,
-                                   root7_d((e_d * 0.1) * rcp_d((double)T_air + 273.15)), p.F);
-#endif
-#else
-#if TFG_R5 & 8
-  // e_air = Hum P_air / (eps100 + ome100 Hum) as e0 + el (the products' and
-  // the quotient's rounding errors carried), then ln(e_air / 6.1121) by one
-  // Newton step from v_log_f32 whose residual is formed from e0 + el exactly
-  const float ph = Hum_sp * P_air, pl = fmaf(Hum_sp, P_air, -ph);
-  const float dh = fmaf(p.f_ome100, Hum_sp, p.f_eps100);
-  const float dl = fmaf(p.f_ome100, Hum_sp, p.f_eps100 - dh) + fmaf(p.f_ome100_lo, Hum_sp, p.f_eps100_lo);
-  float rd = frcp(dh);
-  rd = fmaf(fmaf(-dh, rd, 1.0f), rd, rd);
-  const float e_air = ph * rd;
-  const float el = (fmaf(-e_air, dh, ph) + fmaf(-e_air, dl, pl)) * rd;
-  const float ah = e_air * p.f_c6_hi, al = fmaf(e_air, p.f_c6_hi, -ah);  // e0 / 6.1121 = ah + al
-  const float ly = flog2(ah);
-  const float Ey = fexp2(-ly);
-  const float lr = fmaf(fmaf(e_air, p.f_c6_lo, fmaf(el, p.f_c6_hi, al)), Ey, fmaf(ah, Ey, -1.0f));
-  const float log_term = fmaf(ly, kLn2, lr);
-#elif TFG_R5 & 4
-  float rd = frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
-  rd = fmaf(fmaf(-(p.f_eps100 + p.f_ome100 * Hum_sp), rd, 1.0f), rd, rd);
-  const float e_air = Hum_sp * P_air * rd;
+  const float e_air = Hum_sp * P_air * frcp_nr(p.f_eps100 + p.f_ome100 * Hum_sp);
+  // dew point (:888-893) and surface temperature (:906-910).  ln(e_air /
+  // 6.1121) as the log of the ratio (~1) and Newton-refined: no bias of
+  // v_log_f32 reaches T_dew, which every flux term reads
   const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
-#elif TFG_R5 & 64
-  const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
-  // ln(e_air / 6.1121) with 1/6.1121 as hi + lo and the product's rounding
-  // carried into the Newton residual (no constant or rounding bias)
-  const float ah = e_air * p.f_c6_hi, al = fmaf(e_air, p.f_c6_hi, -ah) + e_air * p.f_c6_lo;
-  const float ly = flog2(ah);
-  const float Ey = fexp2(-ly);
-  const float log_term = fmaf(ly, kLn2, fmaf(al, Ey, fmaf(ah, Ey, -1.0f)));
-#else
-  const float e_air = Hum_sp * P_air * frcp(p.f_eps100 + p.f_ome100 * Hum_sp);
-  // dew point (:888-893) and surface temperature (:906-910)
-  // ln(e_air / 6.1121) as the log of the ratio (~1): v_log_f32's mean error is
-  // -0.44 ulp of its result, so a result near zero keeps that bias negligible,
-  // where log2(e_air) - log2(6.1121) would carry it into T_dew
-  const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
-#endif
-#if TFG_R5 & 4
-  const float dden = 18.678f - log_term;
-  float rdd = frcp(dden);
-  rdd = fmaf(fmaf(-dden, rdd, 1.0f), rdd, rdd);
-  const float T_dew = 257.14f * log_term * rdd;
-#elif TFG_R5 & 64
-  // 257.14 and 18.678 as hi + lo: their fp32 roundings (+5.7e-8, -2.7e-8) were a T_dew bias of ~1e-6 K
-  const float T_dew = fmaf(log_term, 257.14f, log_term * -1.4648438e-05f) *
-                      frcp((18.678f - log_term) + 5.0354004e-07f);
-#else
-  const float T_dew = 257.14f * log_term * frcp(18.678f - log_term);
-#endif
+  const float T_dew = 257.14f * log_term * frcp_nr(18.678f - log_term);
   const float T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
-#endif
   const float RH = e_air * inv_esat;
   // turbulent fluxes (:640-745, :919-934)
-#if !TFG_ACC_DEW
   const float dTs = T_air - T_surf;
-#endif
-#if TFG_ACC_TURB
-  const double dTs_d = (double)dTs;
-  const double TK_d = (double)T_air + 273.15;
-  double bot_d = ((double)uz * (double)uz) * TK_d;
-  if (bot_d == 0.0) bot_d = 0.01;
-  const double Ri_d = p.gz * dTs_d * rcp_d(bot_d);
-  // ln((z - h_snow)/z0) ~ 9: only its relative error reaches Dn, so the fp32
-  // log2 y of the fp32-rounded argument plus its Newton correction c, added
-  // in fp64 (y alone, an fp32 number near 13, is 3.6e-8 off at best)
-  const float la = (float)dmax<NS>((p.z - st.h_snow) * p.inv_z0, 0.01);
-  const float ly = flog2(la);
-  const float lc = fmaf(la, fexp2(-ly), -1.0f) * kLog2e;
-  const double Ln_d = ((double)ly + (double)lc) * 0.69314718055994531;
-  const double Dn_d = (double)uz * (p.kappa * p.kappa) * rcp_d(Ln_d * Ln_d);
-  const double Dh_d = (Ri_d > 0.0) ? Dn_d * rcp_d(fma(10.0, Ri_d, 1.0)) : Dn_d * fma(-10.0, Ri_d, 1.0);
-  const float Dh = (float)Dh_d;
-#else
   float bot = (uz * uz) * T_K;
   if (bot == 0.0f) bot = 0.01f;
-#if TFG_R5 & 16
-  float rb = frcp(bot);
-  rb = fmaf(fmaf(-bot, rb, 1.0f), rb, rb);
-  const float Ri = p.f_gz * dTs * rb;
-#else
   const float Ri = p.f_gz * dTs * frcp(bot);
-#endif
-#if TFG_R5 & 1
-  // log2((z - h_snow)/z0) = ly + k with ly = log2((z - h_snow) 2^-k / z0) ~ 0: squared as ly (ly + 2k) + k^2
+  // log2((z - h_snow)/z0) = ly + k with ly = log2((z - h_snow) 2^-k / z0) ~ 0
+  // (k = round(log2(z/z0)), host side): squared as ly (ly + 2k) + k^2, so
+  // v_log_f32's error is relative to ly, not to the whole log (~13)
   const float ly2 = flog2(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0s, p.f_l2min));
   const float L2sq = fmaf(ly2, ly2 + p.f_l2k2, p.f_l2kk);
-#else
-  const float L2 = flog2_split(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0, 0.01f));
-  const float L2sq = L2 * L2;
-#endif
-#if TFG_R5 & 16
-  float rl = frcp(L2sq);
-  rl = fmaf(fmaf(-L2sq, rl, 1.0f), rl, rl);
-  const float Dn = uz * p.f_k2 * rl;
-  const float d10 = fmaf(10.0f, Ri, 1.0f);
-  float rh = frcp(d10);
-  rh = fmaf(fmaf(-d10, rh, 1.0f), rh, rh);
-  const float Dh = (Ri > 0.0f) ? Dn * rh : Dn * fmaf(-10.0f, Ri, 1.0f);
-#else
   const float Dn = uz * p.f_k2 * frcp(L2sq);
   const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
-#endif
-#endif
   // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
   // (:853), written without the cancellation of the two near-equal pressures:
-  //   e_air - e_surf = -e_air*expm1(x),  x = -k*dTs/((T_s+c)(T_a+c))
-  // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15)
-#if TFG_R5 & 256
-  const float tsc = T_surf + (p.satterlund ? 273.15f : 237.3f);
-  float rS = frcp(tsc);
-  rS = fmaf(fmaf(-tsc, rS, 1.0f), rS, rS);
-#else
-  const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
-#endif
-#ifndef TFG_DE_EXPM1
-#define TFG_DE_EXPM1 0
-#endif
-#if TFG_DE_EXPM1
-  const float xs = (p.satterlund ? -5417.9857f : -4105.29f) * dTs * rS * rA;
-  const float de = -e_air * fexpm1(xs);
-#else
-  // one unbiased exp2 of the exponent difference: the remaining error is
+  //   e_air - e_surf = e_air*(1 - 2^x2),  x2 = -k*log2(e)*dTs/((T_s+c)(T_a+c))
+  // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15):
+  // one unbiased exp2 of the exponent difference, so the remaining error is
   // random (v_exp_f32 rounding), not a bias that would accumulate in Eccs
-  const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;  // k*log2(e)
+  const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
+  const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;
   const float de = fmaf(-e_air, fexp2(xs2), e_air);
-#endif
-#if TFG_ACC_TURB
-  const float Qh = (float)(p.rho_air_Cp_air * Dh_d * dTs_d);
-#else
   const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
-#endif
   const float Qe = p.f_qe * Dh * de * fexp2(g.ek * rT);  // lhc / p0 folded
   // snowfall window + albedo ageing (:1006-1059)
   {
@@ -1367,98 +1136,35 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
     if (dark) K_cs = 0.0f;
   }
   const float Qn_SW = K_cs * (1.0f - albedo);
-  // longwave (:1167-1248)
-  float em_air;
-#if TFG_R5 & 2
-  float em_m1;  // em_air - 1, for the long-wave balance
-#endif
+  // longwave (:1167-1248): em_air - 1 (the balance below needs only that)
+  float em_m1;
   if (!p.satterlund) {
-#if TFG_R5 & 1
-    const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));  // argument ~1: no log bias
-    em_air = fmaf(p.f_ccFs, em_r, p.f_F);
-#if (TFG_R5 & 2) && (TFG_R5 & 128)
-    em_m1 = fmaf(p.f_ccFs, em_r, fmaf(p.f_ccFs_lo, em_r, p.f_Fm1));
-#elif TFG_R5 & 2
-    em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);
-#endif
-#else
-    em_air = fmaf(p.f_ccF, fexp2(flog2_split(e_air * 0.1f * rT) * (1.0f / 7.0f)), p.f_F);
-#if TFG_R5 & 2
-    em_m1 = em_air - 1.0f;
-#endif
-#endif
+    // (e_air / (10 T_K))^(1/7) as (e_air 102.4 / T_K)^(1/7) 2^(-10/7): the
+    // scaled argument is ~1, so v_log_f32's relative error stays off the root
+    const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));
+    em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);  // (1-F) 1.72 (1+0.22C^2) root + F - 1
   } else {
-    em_air = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f)))));
-#if TFG_R5 & 2
-    em_m1 = em_air - 1.0f;
-#endif
+    em_m1 = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f))))) - 1.0f;
   }
-#if TFG_ACC_EM
-  // (e/T)^(1/7) from fp64 e_air and T_K, rounded to fp32 once (:1167)
-#if TFG_ACC_DEW
-  if (!p.satterlund) em_air = em_root;
-#else
-  if (!p.satterlund)
-    em_air = (float)fma(p.one_minus_F_172 * p.cloud_term,
-                        root7_d(((double)e_air * 0.1) * rcp_d((double)T_air + 273.15)), p.F);
-#endif
-#endif
-  const double em_d = (double)em_air;
-#if TFG_ACC_LW
-  const double TK_d2 = (double)T_air + 273.15, tks = (double)T_surf + 273.15;
-  const double a2 = TK_d2 * TK_d2, s2 = tks * tks;
-  const double Qn_LW_d = p.em_surf_sigma * fma(em_d, a2 * a2, -(s2 * s2));
-  const float Qn_LW = (float)Qn_LW_d;
-#elif TFG_LW_SPLIT || (TFG_R5 & 2)
-  // em Ta^4 - Ts^4 without its cancellation (LW_in ~ LW_out ~ 300 W m-2 net
+  // em Ta^4 - Ts^4 without its cancellation (LW_in ~ LW_out ~ 300 W m-2, net
   // ~100): (em - 1) Ta^4 + (Ta - Ts)(Ta + Ts)(Ta^2 + Ts^2), with Ta - Ts the
-  // degC difference dTs (exact of the two fp32 sums' rounding) and em - 1 exact;
-  // the pure-relative misses of SM fall 1.6x in the fp32 emulation
-  // (tests/diagnostics/fp32_emulation.py "lwx"), as with the fp64 balance
+  // degC difference dTs (free of the rounding of the two +273.15 sums)
   const float T_surf_K = T_surf + 273.15f;
   const float ta2 = T_K * T_K;
   const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
-#if (TFG_R5 & 2) && (TFG_R5 & 128)
-  // Ta^4 with Ta = T_air + 273.15 exactly: the fp32 sum's rounding and 273.15f's
-  // (-6.1e-6 K) as lo, Ta^4 = ta^4 (1 + 4 lo / ta): a +-1.5e-5 K error of Ta
-  // was +-2.2e-7 of (em - 1) Ta^4 ~ 75 W m-2
-  const float tlo = ((273.15f - T_K) + T_air) + 6.1035156e-06f;
-  const float t1 = em_m1 * (ta2 * ta2);
-  const float lw = fmaf(t1, 4.0f * tlo * rT, t1) + d4;
-  const float Qn_LW = fmaf(p.f_em_surf_sigma, lw, p.f_esig_lo * lw);
-#elif TFG_R5 & 2
   const float Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
-#else
-  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_air - 1.0f, ta2 * ta2, d4);
-#endif
-  const double Qn_LW_d = (double)Qn_LW;
-#else
-  const float T_surf_K = T_surf + 273.15f;
-  const float ta2 = T_K * T_K, ts2 = T_surf_K * T_surf_K;
-  const float Qn_LW = p.f_em_surf_sigma * fmaf((float)em_d, ta2 * ta2, -(ts2 * ts2));
-  const double Qn_LW_d = (double)Qn_LW;
-#endif
-#if TFG_ACC_SUM  // the flux sum and E_in in fp64
-  double Q_sum = (((double)Qn_SW + Qn_LW_d) + (double)Qh) + (double)Qe;
-  if constexpr (QC) Q_sum = Q_sum + (double)qc;  // :1314, Qc last (Qa = 0)
-#else
   float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
   if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
-#endif
 
   melt_fast<NS>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
-#if defined(TFG_DEBUG_TERM)  // diagnostic builds only: a flux term replaces RH in the output
-  const float dbg[13] = {(float)Q_sum, Qn_SW, Qn_LW, Qh, Qe, T_dew, Dh, dTs, e_air, 0.0f, 0.0f, de, fexp2(g.ek * rT)};
-  o.RH = dbg[TFG_DEBUG_TERM];
-#endif
-#if defined(TFG_DEBUG_TERMS)  // diagnostic builds only (tests/diagnostics/term_attribution.py): the
-                              // step's energy terms replace the six outputs; the state evolves as usual
+#if defined(TFG_DEBUG_TERMS)  // diagnostic builds only (tests/diagnostics/term_bias.py): the step's
+                              // energy terms replace the six outputs; the state evolves as usual
   o.h_snow = Qn_SW;
   o.SM = Qn_LW;
   o.h_ice = Qh;
   o.IM = Qe;
   o.M_total = P_snow > 0.0f ? snowfall_cold(p, P_snow, RH, T_air) : 0.0f;
-  o.RH = (float)Q_sum;
+  o.RH = Q_sum;
 #endif
 }
 
