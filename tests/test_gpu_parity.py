@@ -172,8 +172,8 @@ def test_fp64_engine_vs_reference_fixtures(name):
     errs = {v: float(parity(outs[v], g["outputs"][v], mask=mask)[0]) for v in HIST}
     _report(f"fp64_fixture_{name}", {"max_rel_by_output": errs, "melt_out_flips": rule["flips"],
                                      "fp64_baseline_flips": rule["fp64_flips"]})
-    for v in HIST:
-        assert errs[v] <= 1e-10, v
+    for v in HIST:  # the reference's bar is 1e-10; the engine is held to 1e-12
+        assert errs[v] <= 1e-12, (v, errs[v])
     keep = flip < 0
     assert parity(state["h_swe"], g["outputs"]["h_swe"][-1], mask=keep)[0] <= 1e-10
     assert parity(state["h_iwe"], g["outputs"]["h_iwe"][-1], mask=keep)[0] <= 1e-10
