@@ -10,7 +10,10 @@ sample floor s_v, so the entries that set max_floored_rel can be classified
 on the CPU (depletion steps, melt-out splits, ordinary steps).  Diagnostic
 only.
 
-  python tests/diagnostics/parity_tail.py OUT.npz [top] -- <bench.py arguments>
+  python tests/diagnostics/parity_tail.py OUT.npz [top] [--rank R --world N] -- <bench.py arguments>
+
+With --rank / --world the sample is rank R's of an N-rank bench line (its own
+shard, bench.shard_plan; its parity_plan rows), run here as one process.
 """
 import sys
 import time
@@ -24,7 +27,10 @@ sys.path[:0] = [str(ROOT), str(ROOT / "topoflow-glacier_amd")]
 
 def main():
     out = sys.argv[1]
-    top = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2] != "--" else 256
+    head = sys.argv[:sys.argv.index("--")] if "--" in sys.argv else sys.argv
+    top = int(head[2]) if len(head) > 2 and not head[2].startswith("--") else 256
+    rank = int(head[head.index("--rank") + 1]) if "--rank" in head else 0
+    world = int(head[head.index("--world") + 1]) if "--world" in head else 1
     bargs = sys.argv[sys.argv.index("--") + 1:] if "--" in sys.argv else []
     import bench
 
@@ -37,15 +43,15 @@ def main():
     from topoflow_glacier.engine import GlacierEngine
     from topoflow_glacier.synthetic import diurnal_table
 
-    plan = bench.shard_plan(args, 1, 0)
+    plan = bench.shard_plan(args, world, rank)
     if not args.fuse:
-        args.fuse = bench.auto_fuse(args.ny * args.nx, 8 if args.engine == "float64" else 4)
-    cfg = TopoflowGlacierConfig.model_validate(dict(bench.BASE_CFG, ny=args.ny, nx=args.nx, dt=args.dt))
-    eng = GlacierEngine(cfg, args.ny, args.nx, engine=args.engine, device=0, n_frames=args.frames,
-                        hist_depth=args.fuse, fuse_steps=args.fuse)
+        args.fuse = bench.auto_fuse(plan["rows"] * args.nx, 8 if args.engine == "float64" else 4)
+    cfg = TopoflowGlacierConfig.model_validate(dict(bench.BASE_CFG, ny=plan["rows"], nx=args.nx, dt=args.dt))
+    eng = GlacierEngine(cfg, plan["rows"], args.nx, row0=plan["row0"], engine=args.engine, device=0,
+                        n_frames=args.frames, hist_depth=args.fuse, fuse_steps=args.fuse)
     eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
     t0 = time.perf_counter()
-    cap = bench.capture_parity(eng, args, plan, 1, torch, 0)
+    cap = bench.capture_parity(eng, args, plan, world, torch, 0)
     eng.close()
     print(f"captured {cap['plan']} in {time.perf_counter() - t0:.1f} s", flush=True)
     ref, c64, _, pcfg = bench.oracle_sample(args, cap["plan"], bench._cpu_threads())
@@ -63,7 +69,8 @@ def main():
     w64 = max(float(np.where(cls64.ok, np.abs(c64[v] - ref[v]) / np.maximum(np.maximum(np.abs(ref[v]), floors[v]),
                                                                            1e-300), 0.0).max()) for v in bench.HIST)
     keep = {"cells": cells, "worst": worst[cells], "floors": np.array([floors[v] for v in bench.HIST]),
-            "names": np.array(bench.HIST), "args": np.array(" ".join(bargs)), "ok": cls.ok[:, cells],
+            "names": np.array(bench.HIST), "args": np.array(" ".join(bargs)), "rank": rank, "world": world,
+            "global_rows": np.array([cap["plan"]["row0"], cap["plan"]["row0"] + cap["plan"]["rows"] - 1]), "ok": cls.ok[:, cells],
             "excused": cls.excused[:, cells], "flip": cls.flip[cells], "cut": cls.cut[cells],
             "flip64": cls.flip64[cells], "n_flips": (cls.flip >= 0).sum(), "n_flips64": (cls.flip64 >= 0).sum(),
             "n_excused": cls.excused.sum(), "n_genuine": len(cls.genuine), "n_onsets": len(cls.onset),
