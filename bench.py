@@ -204,6 +204,10 @@ def parse():
                     help="add the queued variant of the per-step grid leg (the same steps set into frames, then one "
                          "fused launch); off by default: its short launches of the timed kernel would enter the "
                          "kernel's rocprof average")
+    ap.add_argument("--dropin-clean", action="store_true",
+                    help="add the clean-form K = 1 launches beside the per-step grid leg (a same-run A/B of the two "
+                         "step forms); off by default: they are launches of the timed kernel instance at K = 1, "
+                         "which would enter its rocprof average")
     ap.add_argument("--dropin-instances", type=int, default=4096,
                     help="single-catchment BMI models of the defer_update leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -648,23 +652,27 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
            "protocol": "per step: tfg_set_inputs (device f32 [5][n]) + tfg_step(1)" + (
                f"; queued: the same inputs into {steps} frames, then one {steps}-step launch" if args.dropin_queued
                else "")}
-    # first the same K = 1 launches in the clean step form, for a same-run A/B of the two forms at 184 B per
-    # cell-update: the frames as fill_synthetic wrote them (known finite), no inputs set, each launch between
-    # HIP events (before the per-step protocol, whose device-set inputs leave the frames of unknown status)
-    ns0 = eng.nan_safe_launches()
-    ev_c = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    torch.cuda.synchronize(eng.device)
-    for s in range(steps):
-        ev_c[s][0].record(stream)
-        eng.run(1)
-        ev_c[s][1].record(stream)
-    torch.cuda.synchronize(eng.device)
-    c_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_c]))
-    out["clean_form_step_launch"] = {
-        "step_launch_ms": c_ms, "nan_safe_launches": eng.nan_safe_launches() - ns0,
-        "step_launch_GBps": n * (step_b + launch_b) / (c_ms / 1e3) / 1e9,
-        "note": "per_step's launches read device-set inputs and run the NaN-safe form (device data is not known to "
-                "be finite without a host wait); these read host-checked frames and run the clean form"}
+    # --dropin-clean: first the same K = 1 launches in the clean step form, for a same-run A/B of the two forms
+    # at 184 B per cell-update: the frames as fill_synthetic wrote them (known finite), no inputs set, each launch
+    # between HIP events (before the per-step protocol, whose device-set inputs leave the frames of unknown
+    # status).  Off by default: they are launches of the timed kernel instance at K = 1, which would enter its
+    # rocprof average (profiles/r5_dropin_form_ab.json holds the A/B)
+    c_ms = None
+    if args.dropin_clean:
+        ns0 = eng.nan_safe_launches()
+        ev_c = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize(eng.device)
+        for s in range(steps):
+            ev_c[s][0].record(stream)
+            eng.run(1)
+            ev_c[s][1].record(stream)
+        torch.cuda.synchronize(eng.device)
+        c_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_c]))
+        out["clean_form_step_launch"] = {
+            "step_launch_ms": c_ms, "nan_safe_launches": eng.nan_safe_launches() - ns0,
+            "step_launch_GBps": n * (step_b + launch_b) / (c_ms / 1e3) / 1e9,
+            "note": "per_step's launches read device-set inputs and run the NaN-safe form (device data is not known "
+                    "to be finite without a host wait); these read host-checked frames and run the clean form"}
     for mode in ("per_step", "queued") if args.dropin_queued else ("per_step",):
         ns0 = eng.nan_safe_launches()
         ev_k = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -700,7 +708,8 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
                                      "bytes_per_cell_update_with_input_copy"] / (dev_ms / steps / 1e3) / 1e9
         rec["frac"] = rec["device_GBps"] / HBM_PEAK_GBS
         out[mode] = rec
-    out["clean_form_step_launch"]["nan_safe_over_clean"] = out["per_step"]["step_launch_ms"] / c_ms
+    if c_ms is not None:
+        out["clean_form_step_launch"]["nan_safe_over_clean"] = out["per_step"]["step_launch_ms"] / c_ms
     del blk
     return out
 

@@ -297,8 +297,8 @@ int tfg_set_step_form(tfg_handle* h, int form);
  * same device functions the engine's steps call; and the fp64 engine's exp,
  * log and constant-divisor division (csrc/tfg_fastmath.hpp): exp_k (3), the
  * device libm's exp (4), log_k (5), the device libm's log (6), x / 6.1121 (7)
- * and x / 3600 (8) by div_k, exp_ks (9: exp_k with its constants in
- * scalar registers), fdiv(x, 7.3) (10) and fdiv(7.3, x) (11).  Host arrays of
+ * and x / 3600 (8) by div_k, exp_kv (9: exp_k with its constants in
+ * vector registers), fdiv(x, 7.3) (10) and fdiv(7.3, x) (11).  Host arrays of
  * n values, synchronous. */
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out);
 

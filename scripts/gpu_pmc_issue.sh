@@ -20,6 +20,7 @@ SQ_WAVES SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_IN
 PASSES
 }
 mkdir -p $OUT/f32 $OUT/f64
-run f32 --ny 8192 --nx 8192 --steps 96 --warmup 96 --fuse 96 --no-cpu-baseline || exit 1
-run f64 --engine float64 --ny 4096 --nx 4096 --steps 48 --warmup 24 --fuse 24 --no-cpu-baseline || exit 1
-python3 scripts/issue_summary.py $OUT
+# the bench shapes (128-step launches at 8192^2, 192 at 4096^2 for fp64), timed launches only
+run f32 --ny 8192 --nx 8192 --steps 256 --warmup 128 --fuse 128 --no-cpu-baseline --no-parity --no-dropin || exit 1
+run f64 --engine float64 --ny 4096 --nx 4096 --steps 384 --warmup 192 --fuse 192 --no-cpu-baseline --no-parity --no-dropin || exit 1
+python3 scripts/issue_summary.py $OUT 128 192

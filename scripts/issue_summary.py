@@ -3,7 +3,7 @@ counts of the fused kernel for each engine, and the share of SIMD time the
 vector pipe was issuing (SQ_ACTIVE_INST_VALU, quad-cycles summed over waves,
 against GRBM_GUI_ACTIVE x 1024 SIMDs; MI355X_MICROARCH.md: SQ cycle counters
 count quad-cycles).
-  python3 scripts/issue_summary.py <dir>"""
+  python3 scripts/issue_summary.py <dir> [f32_fuse f64_fuse]"""
 import csv
 import glob
 import json
@@ -13,8 +13,11 @@ from collections import defaultdict
 SIMDS = 256 * 4
 d = sys.argv[1]
 res = {}
-for name, kern, cells, fuse in (("f32", "k_fused<float, false, false", 8192 * 8192, 96),
-                                ("f64", "k_fused<double, true, false", 4096 * 4096, 24)):
+# the timed instances only (the NaN-safe and other forms have other template arguments); the runs carry no
+# parity or drop-in legs, so every dispatch of these is a whole `fuse`-step launch
+F32_FUSE, F64_FUSE = (int(a) for a in (sys.argv[2:4] if len(sys.argv) > 3 else (128, 192)))
+for name, kern, cells, fuse in (("f32", "k_fused<float, false, false, false, false, 1, false>", 8192 * 8192, F32_FUSE),
+                                ("f64", "k_fused<double, true, false, false, false, 1, false>", 4096 * 4096, F64_FUSE)):
     raw = defaultdict(list)
     for f in sorted(glob.glob(f"{d}/{name}/p*/run_counter_collection.csv")):
         per = defaultdict(lambda: defaultdict(float))

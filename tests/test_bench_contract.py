@@ -144,7 +144,7 @@ def test_weak_scaling_stays_behind_its_flag():
 def test_bench_prints_one_json_line_with_the_contract_keys():
     cmd = [sys.executable, str(ROOT / "bench.py"), "--ny", "256", "--nx", "1024", "--steps", "48", "--warmup", "24",
            "--fuse", "24", "--cpu-cells", "4096", "--cpu-steps", "48", "--parity-cells", "2048",
-           "--dropin-instances", "64", "--dropin-queued"]
+           "--dropin-instances", "64", "--dropin-queued", "--dropin-clean"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

@@ -580,7 +580,7 @@ __global__ void k_selftest_powers(const double* __restrict__ x, double* __restri
       case 5: r = tfg_fm::log_k(v); break;
       case 6: r = log(v); break;
       case 7: r = tfg_fm::div_k(v, 6.1121, 1.0 / 6.1121); break;
-      case 9: r = tfg_fm::exp_ks(v); break;
+      case 9: r = tfg_fm::exp_kv(v); break;
       case 10: r = tfg_fm::fdiv(v, 7.3); break;
       case 11: r = tfg_fm::fdiv(7.3, v); break;
       default: r = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;

@@ -20,19 +20,23 @@
 //                  FMAs, v_div_fmas, v_div_fixup).
 //   exp_k(x)       the device libm's exp restated operation for operation
 //                  (Cody-Waite reduction, degree-12 polynomial, ldexp, the same
-//                  overflow/underflow selects): the same results bit for bit
-//                  and the same cost, so that the host build below computes
-//                  exactly what the device does.
+//                  overflow/underflow selects, here behind one test of |x|):
+//                  the same results bit for bit, so that the host build below
+//                  computes exactly what the device does.
+//   fdiv(x, y)     x / y for a variable y: reciprocal, one Newton step, one
+//                  correction of the quotient (within 1 ulp; round 5: one
+//                  Newton step fewer than IEEE-exactness needs, +3.1 %).
 //
 // Same-box A/B at 4096^2 (scripts/gpu_ab_f64.sh, profiles/r3f_ab_f64.log):
 // 26.6 -> 31.2 G cell-updates/s (+17 %).  Holding exp's polynomial
 // coefficients in SGPRs at every call site (the scalar operand of v_fma_f64
 // instead of a v_mov pair feeding v_fmac_f64) saves ~60 more VALU instructions
 // of the step but raises it from 118 to 144 VGPRs (3 instead of 4 waves per
-// SIMD): 29.5 (profiles/r3e_ab_f64.log).  So exp_ks (SGPR constants) is used
-// only at the call sites that leave the step's VGPR count alone (em_air's
-// root, both saturation pressures), exp_k elsewhere; log_k's constants are
-// always scalar operands.  A table-driven exp (2^(j/64) from LDS or from a
+// SIMD): 29.5 (profiles/r3e_ab_f64.log).  Round 5, with the rest of the step
+// leaner, SGPR constants at every exp call site keep it at 128 VGPRs (4 waves)
+// and gain 0.9 % (profiles/r5_ab_f64.json), so exp_k holds them in SGPRs
+// everywhere (exp_kv, the VGPR form, stays for the device test that both give
+// the same bits); log_k's constants are always scalar operands.  A table-driven exp (2^(j/64) from LDS or from a
 // 1 KB global table, degree-5 expm1; within 1 ulp of numpy's) was measured and
 // dropped: it raised the step to 152 VGPRs and its static VALU count
 // (2430 -> 2450), and a global table load shares vmcnt with the step's forcing
@@ -67,6 +71,15 @@
 
 
 namespace tfg_fm {
+
+// A branch the compiler must keep (an empty volatile asm cannot be speculated
+// into a select): for rare special-value fix-ups, which then cost one compare
+// and a skipped branch instead of their selects on every call.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TFG_FM_RARE() asm volatile("")
+#else
+#define TFG_FM_RARE() ((void)0)
+#endif
 
 // d = a * b + c with b (fma_vsv) or c (fma_vvs) a wave-uniform constant held in
 // an SGPR pair.  Host: std::fma.
@@ -108,7 +121,7 @@ TFG_FM_HD inline double bits_to_double(uint64_t b) {
 // SGPR = true: the polynomial coefficients and reduction constants as the
 // scalar operand of v_fma_f64 (SALU moves beside the vector pipe, ~10 fewer
 // VALU instructions), where the call site's register pressure allows it
-// (exp_ks; the others exp_k): the same results either way.
+// (exp_k; exp_kv holds them in VGPRs): the same results either way.
 template <bool SGPR>
 TFG_FM_HD inline double fk(double a, double b, double c) {  // b constant
   if constexpr (SGPR) return fma_vsv(a, b, c);
@@ -142,12 +155,16 @@ TFG_FM_HD inline double exp_impl(double x) {
   const int k = (int)std::fmin(std::fmax(dn, -2147483648.0), 2147483647.0);
 #endif
   double z = std::ldexp(p, k);
-  z = (x > 1024.0) ? (double)INFINITY : z;
-  z = (x < -1075.0) ? 0.0 : z;
+  // overflow, underflow, +-inf and NaN (rare): one test on the common path
+  if (__builtin_expect(!(std::fabs(x) <= 708.0), 0)) {
+    TFG_FM_RARE();
+    z = (x > 1024.0) ? (double)INFINITY : z;
+    z = (x < -1075.0) ? 0.0 : z;
+  }
   return z;
 }
-TFG_FM_HD inline double exp_k(double x) { return exp_impl<false>(x); }
-TFG_FM_HD inline double exp_ks(double x) { return exp_impl<true>(x); }
+TFG_FM_HD inline double exp_k(double x) { return exp_impl<true>(x); }
+TFG_FM_HD inline double exp_kv(double x) { return exp_impl<false>(x); }
 
 // ---------------------------------------------------------------------------
 // log: fdlibm e_log.c's reduction and polynomial (Lg1..Lg7), one formula for
@@ -189,11 +206,15 @@ TFG_FM_HD inline double log_k(double x) {
   const double R = t2 + t1;
   const double hfsq = 0.5 * f * f;
   const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-  const double y = fma_vsv(dk, ln2_hi, -((hfsq - fma_vv(s, hfsq + R, dk * ln2_lo)) - f));
-  // special values: log(+-0) = -inf, log(x < 0) = NaN, log(+inf) = +inf; NaN propagates through the above
-  if (x == 0.0) return -(double)INFINITY;
-  if (x < 0.0) return (double)NAN;
-  if (x == (double)INFINITY) return x;
+  double y = fma_vsv(dk, ln2_hi, -((hfsq - fma_vv(s, hfsq + R, dk * ln2_lo)) - f));
+  // special values (rare: one test on the common path): log(+-0) = -inf, log(x < 0) = NaN,
+  // log(+inf) = +inf; NaN propagates through the above
+  if (__builtin_expect(!(x > 0.0 && x < (double)INFINITY), 0)) {
+    TFG_FM_RARE();
+    y = (x == 0.0) ? -(double)INFINITY : y;
+    y = (x < 0.0) ? (double)NAN : y;
+    y = (x == (double)INFINITY) ? x : y;
+  }
   return y;
 }
 
@@ -212,18 +233,18 @@ TFG_FM_HD inline double div_k(double x, double c, double rc) {
 }
 
 // ---------------------------------------------------------------------------
-// x / y for a variable y: the reciprocal from rcp_approx and two Newton steps,
-// q = RN(x r), and one correction q + (x - q y) r -- IEEE's quotient but for
-// rare last-bit cases (tests/test_fastmath.py: within 1 ulp of numpy's), 8 VALU
-// instead of the 11 of the general sequence (v_div_scale x2, v_rcp, five
-// FMAs, v_div_fmas, v_div_fixup).  For finite x and finite nonzero y (every
+// x / y for a variable y: the reciprocal from rcp_approx and one Newton step
+// (relative error ~2^-46 from either seed), q = RN(x r), and one correction
+// q + (x - q y) r, whose error is that of r times |q - x/y| -- IEEE's quotient
+// but for rare last-bit cases (tests/test_fastmath.py: within 1 ulp of numpy's,
+// equal in > 99.9 %), 6 VALU instead of the 11 of the general sequence
+// (v_div_scale x2, v_rcp, five FMAs, v_div_fmas, v_div_fixup).  For finite x and finite nonzero y (every
 // quotient of the physics); NaN propagates.  A zero or infinite operand gives
 // NaN, where IEEE gives inf or 0: the fp64 step never divides by them.
 // ---------------------------------------------------------------------------
 TFG_FM_HD inline double fdiv(double x, double y) {
   TFG_FM_NO_CONTRACT
   double r = rcp_approx(y);
-  r = fma_vv(fma_vv(-y, r, 1.0), r, r);
   r = fma_vv(fma_vv(-y, r, 1.0), r, r);
   const double q = x * r;
   return fma_vv(fma_vv(-q, y, x), r, q);

@@ -27,7 +27,6 @@ namespace tfg {
 using tfg_fm::div_k;
 using tfg_fm::fdiv;
 using tfg_fm::exp_k;
-using tfg_fm::exp_ks;
 using tfg_fm::log_k;
 
 // Earth_Angular_Velocity() (SF:252) [rad/h] and its correctly rounded
@@ -475,7 +474,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // saturation vapour pressure (air) :788-802
   double e_sat_air;
   if (!p.satterlund) {
-    e_sat_air = 0.611 * exp_ks(fdiv(17.3 * T_air, T_air + 237.3));
+    e_sat_air = 0.611 * exp_k(fdiv(17.3 * T_air, T_air + 237.3));
   } else {
     e_sat_air = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1000.0, 1.0 / 1000.0);
   }
@@ -492,7 +491,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
   double e_sat_surf;
   if (!p.satterlund) {
-    e_sat_surf = 0.611 * exp_ks(fdiv(17.3 * T_surf, T_surf + 237.3));
+    e_sat_surf = 0.611 * exp_k(fdiv(17.3 * T_surf, T_surf + 237.3));
   } else {
     e_sat_surf = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
   }
@@ -543,7 +542,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     const double term1 = p3.one_minus_F_172 * root7(fdiv(div_k(e_air, 10.0, 1.0 / 10.0), T_air_K));
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
-    em_air = 1.08 * (1.0 - exp_ks(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
+    em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
