@@ -31,7 +31,7 @@ HEADER = ROOT / "topoflow-glacier_amd" / "csrc" / "tfg_fastmath.hpp"
 EXP, EXP_LIBM, LOG, LOG_LIBM, DIV_61121, DIV_3600, EXP_VGPR, FDIV_BY_73, FDIV_73_BY = 3, 4, 5, 6, 7, 8, 9, 10, 11
 
 # the bounds HISTORY.md section 5 states (ulps of numpy's result)
-EXP_ULPS = 1.0
+EXP_ULPS = 3.0  # degree-10 polynomial since round 5 (the device libm's degree 12: 1 ulp)
 LOG_ULPS = 1.0
 
 
@@ -132,7 +132,7 @@ def test_variable_division_within_one_ulp(host):
     # may differ from IEEE's; no comparison or select of the step reads it)
 
 
-def test_exp_within_one_ulp_of_numpy(host):
+def test_exp_within_three_ulp_of_numpy(host):
     ev, _ = host
     rng = np.random.default_rng(12)
     worst = {}
@@ -172,14 +172,15 @@ def _device(x, which):
 @pytest.mark.gpu
 def test_fastmath_on_the_device(host):
     """The device computes what the host build computes, bit for bit; its exp_k
-    (its constants in scalar registers; exp_kv, the same in vector registers) equals the
-    device libm's exp bit for bit; its log_k is within 1 ulp of the device
-    libm's log."""
+    (its constants in scalar registers; exp_kv, the same in vector registers) is within
+    3 ulp of the device libm's exp; its log_k is within 1 ulp of the device libm's log."""
     ev, _ = host
     rng = np.random.default_rng(14)
     xe = np.concatenate([*exp_arguments(rng), SPECIAL])
     assert _same(_device(xe, EXP), ev(xe, EXP))
-    assert _same(_device(xe, EXP), _device(xe, EXP_LIBM))
+    got, libm = _device(xe, EXP), _device(xe, EXP_LIBM)
+    fin = np.isfinite(libm) & (libm > 0)
+    assert _ulps(got[fin], libm[fin]).max() <= EXP_ULPS and _same(got[~fin], libm[~fin])
     assert _same(_device(xe, EXP_VGPR), _device(xe, EXP))
     xl = np.concatenate([*log_arguments(rng), SPECIAL])
     got = _device(xl, LOG)

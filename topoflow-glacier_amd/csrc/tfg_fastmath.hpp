@@ -18,11 +18,13 @@
 //                  random pairs and the engine's divisors); 6 VALU instead of
 //                  the 11 of the general sequence (v_div_scale x2, v_rcp, five
 //                  FMAs, v_div_fmas, v_div_fixup).
-//   exp_k(x)       the device libm's exp restated operation for operation
-//                  (Cody-Waite reduction, degree-12 polynomial, ldexp, the same
-//                  overflow/underflow selects, here behind one test of |x|):
-//                  the same results bit for bit, so that the host build below
-//                  computes exactly what the device does.
+//   exp_k(x)       the device libm's exp restated (Cody-Waite reduction, ldexp,
+//                  the same overflow/underflow selects, here behind one test of
+//                  |x|) with a degree-10 polynomial where the libm's is degree
+//                  12: within 3 ulp of numpy's (round 5), and the host build
+//                  below computes exactly what the device does.
+//   div_r(x, rc)   x / c as x * RN(1/c), within 1 ulp: every constant divisor
+//                  whose last bit no melt-out gate reads (round 5).
 //   fdiv(x, y)     x / y for a variable y: reciprocal, one Newton step, one
 //                  correction of the quotient (within 1 ulp; round 5: one
 //                  Newton step fewer than IEEE-exactness needs, +3.1 %).
@@ -116,7 +118,8 @@ TFG_FM_HD inline double bits_to_double(uint64_t b) {
 
 // ---------------------------------------------------------------------------
 // exp: the device libm's exp (ROCm 7.2 device libs) as the compiler emits it
-// for this engine (the constants below are read off its machine code).
+// for this engine (reduction constants read off its machine code), with a
+// degree-10 polynomial fitted on [-ln2/2, ln2/2] (round 5) for its degree 12.
 // ---------------------------------------------------------------------------
 // SGPR = true: the polynomial coefficients and reduction constants as the
 // scalar operand of v_fma_f64 (SALU moves beside the vector pipe, ~10 fewer
@@ -138,15 +141,15 @@ TFG_FM_HD inline double exp_impl(double x) {
   const double dn = std::rint(x * bits_to_double(0x3ff71547652b82feull));  // x / ln 2
   double t = fk<SGPR>(dn, bits_to_double(0xbfe62e42fefa39efull), x);              // - dn ln2_hi
   t = fk<SGPR>(dn, bits_to_double(0xbc7abc9e3b39803full), t);                     // - dn ln2_lo
-  double p = fp<SGPR>(t, bits_to_double(0x3e5ade156a5dcb37ull), bits_to_double(0x3e928af3fca7ab0cull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3ec71dee623fde64ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3efa01997c89e6b0ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3f2a01a014761f6eull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3f56c16c1852b7b0ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3f81111111122322ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3fa55555555502a1ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3fc5555555555511ull));
-  p = fp<SGPR>(t, p, bits_to_double(0x3fe000000000000bull));
+  // degree 10 (round 5; the device libm's is 12): within 3 ulp of numpy's exp
+  double p = fp<SGPR>(t, 0x1.2677102fbfba0p-22, 0x1.72ea1106c32a0p-19);
+  p = fp<SGPR>(t, p, 0x1.a01c31bed4303p-16);
+  p = fp<SGPR>(t, p, 0x1.a0198c587737fp-13);
+  p = fp<SGPR>(t, p, 0x1.6c16c077e694ap-10);
+  p = fp<SGPR>(t, p, 0x1.11111126084c0p-7);
+  p = fp<SGPR>(t, p, 0x1.55555555a61c8p-5);
+  p = fp<SGPR>(t, p, 0x1.555555555059ap-3);
+  p = fp<SGPR>(t, p, 0x1.ffffffffffdf2p-2);
   p = fma_vv(t, p, 1.0);
   p = fma_vv(t, p, 1.0);
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -230,6 +233,16 @@ TFG_FM_HD inline double div_k(double x, double c, double rc) {
   const double e = fma_vv(-q, c, x);
   const double q1 = fma_vv(e, rc, q);
   return (e < 0.0 || e > 0.0) ? q1 : q;
+}
+
+// x / c for a constant c as x * RN(1/c): within 1 ulp of the quotient, 1 VALU.
+// For every division by a model constant whose last bit does not decide a
+// melt-out gate (round 5: the fp64 engine is held to 1e-12 of the reference,
+// not to its last bit); div_k keeps the correctly rounded quotient where the
+// reference's h - (h/3600) dt 3600 residual is read by an exact-zero test.
+TFG_FM_HD inline double div_r(double x, double rc) {
+  TFG_FM_NO_CONTRACT
+  return x * rc;
 }
 
 // ---------------------------------------------------------------------------

@@ -25,6 +25,7 @@
 namespace tfg {
 
 using tfg_fm::div_k;
+using tfg_fm::div_r;
 using tfg_fm::fdiv;
 using tfg_fm::exp_k;
 using tfg_fm::log_k;
@@ -263,7 +264,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   // update_snow_meltrate :1364-1373
   double E_in = Q_sum * dt;
   double E_rem = npmax(E_in - st.Eccs, 0.0);
-  double SM = div_k(div_k(E_rem, dt, p.inv_dt), p.rho_H2O_Lf, p.inv_rho_H2O_Lf);
+  double SM = div_r(div_r(E_rem, p.inv_dt), p.inv_rho_H2O_Lf);
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
   SM = npmax(SM, 0.0);
@@ -284,7 +285,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   }
   // update_ice_meltrate :1418-1434
   E_rem = npmax(E_in - st.Ecci, 0.0);
-  double IM = div_k(div_k(E_rem, dt, p.inv_dt), p.rho_H2O_Lf, p.inv_rho_H2O_Lf);
+  double IM = div_r(div_r(E_rem, p.inv_dt), p.inv_rho_H2O_Lf);
   IM = npmax(IM, 0.0);
   IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
   double Ecci = npmax(st.Ecci - E_in, 0.0);
@@ -300,7 +301,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   double h_iwe = st.h_iwe - IM * dt * 3600.0;
   h_iwe = npmax(h_iwe, 0.0);
   // update_combined_meltrate :1441-1443
-  const double M_total = IM + SM + div_k(P_rain, 3600.0, 1.0 / 3600.0);
+  const double M_total = IM + SM + div_r(P_rain, 1.0 / 3600.0);
   // update_snow_depth :1711 / update_ice_depth :1726
   const double h_snow = h_swe * p.ws;
   const double h_ice = h_iwe * p.wi;
@@ -460,7 +461,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556
   const double T_K = T_air + 273.15;
   double p0 = p.sea_p0 * exp_k(fdiv(p.negM_g * s.elev, p.R * T_K));
-  p0 = div_k(p0, 1000.0, 1.0 / 1000.0);
+  p0 = div_r(p0, 1.0 / 1000.0);
   p0 = p0 * 10.0;
   // :567, :576, :585, :604, :613, :623
   const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
@@ -476,16 +477,16 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (!p.satterlund) {
     e_sat_air = 0.611 * exp_k(fdiv(17.3 * T_air, T_air + 237.3));
   } else {
-    e_sat_air = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1000.0, 1.0 / 1000.0);
+    e_sat_air = div_r(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1.0 / 1000.0);
   }
   e_sat_air = e_sat_air * 10.0;
   // :817-826
   double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
-  e = div_k(e, 1000.0, 1.0 / 1000.0);
+  e = div_r(e, 1.0 / 1000.0);
   const double e_air = e * 10.0;
   const double RH = fdiv(e_air, e_sat_air);  // :838
   // :888-893
-  const double log_term = log_k(div_k(e_air, 6.1121, 1.0 / 6.1121));
+  const double log_term = log_k(div_r(e_air, 1.0 / 6.1121));
   const double T_dew = fdiv(257.14 * log_term, 18.678 - log_term);
   // :906-910 (previous-step depths)
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
@@ -493,7 +494,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (!p.satterlund) {
     e_sat_surf = 0.611 * exp_k(fdiv(17.3 * T_surf, T_surf + 237.3));
   } else {
-    e_sat_surf = div_k(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15)), 1000.0, 1.0 / 1000.0);
+    e_sat_surf = div_r(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15)), 1.0 / 1000.0);
   }
   e_sat_surf = e_sat_surf * 10.0;
   // :640-644, per cell
@@ -502,7 +503,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   if (bot == 0.0) bot = 0.01;
   const double Ri = fdiv(top, bot);
   // :670-726
-  const double arg = fdiv(p.kappa, log_k(npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01)));
+  const double arg = fdiv(p.kappa, log_k(npmax(div_r(p.z - h_snow, p.inv_z0), 0.01)));
   const double Dn = uz * (arg * arg);
   const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
   // :744-745
@@ -539,10 +540,10 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * root7(fdiv(div_k(e_air, 10.0, 1.0 / 10.0), T_air_K));
+    const double term1 = p3.one_minus_F_172 * root7(fdiv(div_r(e_air, 1.0 / 10.0), T_air_K));
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
-    em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_k(T_air_K, 2016.0, 1.0 / 2016.0))));
+    em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_r(T_air_K, 1.0 / 2016.0))));
   }
   // :1231-1248
   const double T_surf_K = T_surf + 273.15;
@@ -636,7 +637,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   d.PS += P_snow * p.da_m2 * dt;
   // :817-826
   double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
-  e = div_k(e, 1000.0, 1.0 / 1000.0);
+  e = div_r(e, 1.0 / 1000.0);
   const double e_air = e * 10.0;
   const double T_air_K = T_air + 273.15;
   // window and days since snowfall (:1023-1040), ahead of the albedo exp
@@ -654,11 +655,11 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     ex1 = exp_k(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
   }
   if (X.mine(X_LOG1))  // :670, :888
-    lg1 = log_k(lane == 1 ? npmax(div_k(p.z - h_snow, p.z0, p.inv_z0), 0.01) : div_k(e_air, 6.1121, 1.0 / 6.1121));
+    lg1 = log_k(lane == 1 ? npmax(div_r(p.z - h_snow, p.inv_z0), 0.01) : div_r(e_air, 1.0 / 6.1121));
   if (X.mine(X_TRIG1)) ac = acos(npmin(npmax(-1.0, -1.0 * s.tan_eq * u.tan_d), 1.0));  // SF:325 (one argument)
   cos_wl = cos_hour_angle(s, u);                                                          // SF:867
   if (X.mine(X_POW1) && p.satterlund)  // e_air^(T/2016) (:1190), 10^(...) of e_sat_air (:796)
-    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - fdiv(2353.0, T_air + 273.15) : div_k(T_air_K, 2016.0, 1.0 / 2016.0));
+    pw1 = pow(lane == 2 ? 10.0 : e_air, lane == 2 ? 11.4 - fdiv(2353.0, T_air + 273.15) : div_r(T_air_K, 1.0 / 2016.0));
   X.put(X_EXP1, ex1);
   X.put(X_LOG1, lg1);
   X.put(X_TRIG1, ac);
@@ -672,10 +673,10 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
 
   // :551-556
   double p0 = p.sea_p0 * e_p0;
-  p0 = div_k(p0, 1000.0, 1.0 / 1000.0);
+  p0 = div_r(p0, 1.0 / 1000.0);
   p0 = p0 * 10.0;
   // :788-802, :838
-  double e_sat_air = !p.satterlund ? 0.611 * e_es : div_k(pw_es, 1000.0, 1.0 / 1000.0);
+  double e_sat_air = !p.satterlund ? 0.611 * e_es : div_r(pw_es, 1.0 / 1000.0);
   e_sat_air = e_sat_air * 10.0;
   const double RH = fdiv(e_air, e_sat_air);
   // :888-893, :906-910
@@ -719,7 +720,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   X.put(X_POW2, pw2);
   X.put(X_ATAN2, at2);
   if (W > 1) lds_level_barrier();
-  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : div_k(X.get(X_POW2, pw2, 0), 1000.0, 1.0 / 1000.0);
+  double e_sat_surf = !p.satterlund ? 0.611 * X.get(X_EXP2, ex2, 0) : div_r(X.get(X_POW2, pw2, 0), 1.0 / 1000.0);
   e_sat_surf = e_sat_surf * 10.0;
   const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
@@ -748,7 +749,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :1167-1192, :1231-1248
   double em_air;
   if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * root7(fdiv(div_k(e_air, 10.0, 1.0 / 10.0), T_air_K));
+    const double term1 = p.one_minus_F_172 * root7(fdiv(div_r(e_air, 1.0 / 10.0), T_air_K));
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
