@@ -508,8 +508,6 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
   // :744-745
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
-  // :919-920
-  const double W_p = 1.12 * exp_k(0.0614 * T_dew);
   // :853 (SURFACE uses the air RH)
   const double e_surf = RH * e_sat_surf;
   // :931-934
@@ -519,21 +517,28 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   st.tot_q += window_tot(q_new) - window_tot(q_old);
   const double albedo = albedo_step(p, st, T_air);
   const DevParams& p2 = params();  // Clear_Sky_Radiation phase
-  // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted)
-  const double a_sa = -0.1240 - (0.0207 * W_p);
-  const double b_sa = -0.0682 - (0.0248 * W_p);
-  const double tau = npmin(npmax(exp_k(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
-  const double cos_wl = cos_hour_angle(s, u);  // SF:867
-  double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos_wl + s.sin_leq * u.sin_d);
-  K_ET = npmax(K_ET, 0.0);
-  const double a_s = -0.0363 - (0.0084 * W_p);
-  const double b_s = -0.0572 - (0.0173 * W_p);
-  const double gam_s = (1.0 - exp_k(a_s + (b_s * u.m_opt))) + p2.dust;
-  const double K_dif = 0.5 * gam_s * u.k_et_flat;
-  const double K_global = tau * u.k_et_flat + K_dif;
-  const double K_bs = 0.5 * gam_s * albedo * K_global;
-  double K_cs = (tau * K_ET) + K_dif + K_bs;
-  if (sun_down(p2, s, u, cos_wl)) K_cs = 0.0;
+  // Clear_Sky_Radiation SF:904-941 (uniform parts hoisted), only while the sun
+  // is up on a flat surface this step: flat_dark (a step uniform) makes every
+  // cell dark, K_cs = 0 in the reference too, so half the steps skip W_p
+  // (:919-920), tau and gam_s
+  double K_cs = 0.0;
+  if (!u.flat_dark) {
+    const double W_p = 1.12 * exp_k(0.0614 * T_dew);  // :919-920
+    const double a_sa = -0.1240 - (0.0207 * W_p);
+    const double b_sa = -0.0682 - (0.0248 * W_p);
+    const double tau = npmin(npmax(exp_k(a_sa + (b_sa * u.m_opt)) - p2.dust, 0.0), 1.0);
+    const double cos_wl = cos_hour_angle(s, u);  // SF:867
+    double K_ET = u.isc_e0 * ((u.cos_d * s.cos_leq) * cos_wl + s.sin_leq * u.sin_d);
+    K_ET = npmax(K_ET, 0.0);
+    const double a_s = -0.0363 - (0.0084 * W_p);
+    const double b_s = -0.0572 - (0.0173 * W_p);
+    const double gam_s = (1.0 - exp_k(a_s + (b_s * u.m_opt))) + p2.dust;
+    const double K_dif = 0.5 * gam_s * u.k_et_flat;
+    const double K_global = tau * u.k_et_flat + K_dif;
+    const double K_bs = 0.5 * gam_s * albedo * K_global;
+    K_cs = (tau * K_ET) + K_dif + K_bs;
+    if (sun_down(p2, s, u, cos_wl)) K_cs = 0.0;
+  }
   const double Qn_SW = K_cs * (1.0 - albedo);  // :1139
   const DevParams& p3 = params();  // long-wave and net flux phase
   // update_em_air :1167-1192
@@ -570,7 +575,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const DevParams& p4 = params();  // melt and mass phase
   melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
-  { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_ET, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
+  { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_cs, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
 #endif
 }
 
@@ -1106,34 +1111,40 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
     st.albedo = (double)a;
     albedo = a;
   }
-  // clear-sky shortwave (SF:904-941); W_p = 1.12*w
-  const float w = fexp2((0.0614f * kLog2e) * T_dew);
-  const float tau = nmin<NS>(nmax<NS>(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);  // SF:614
-  const float gam_s = p.f_1pdust - fexp2(fmaf(u.gam_c1, w, u.gam_c0));
-  // cos(lat_eq)*cos(omega*th + dlon)
-  const float cwl = u.cos_wth_f * g.cc - u.sin_wth_f * g.cs;
-  // SF:887; the geometry planes are never NaN (derive_geo maps a NaN slope or
-  // aspect to the reference's 0), so IEEE max is exact here in both forms
-  const float K_ET = fmaxf(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);
-  const float kf = u.k_et_flat_f;
-  const float K_dif = 0.5f * gam_s * kf;
-  const float K_bs = 0.5f * gam_s * albedo * fmaf(tau, kf, K_dif);
-  float K_cs = tau * K_ET + K_dif + K_bs;
-  // dark (SF:939-941): with x = omega*th + dlon and ac = acos(clip(-tan(lat_eq) tan(d))),
-  // th <= T_sr or th >= T_ss  <=>  flat_dark or |x| >= ac
-  //                           <=>  flat_dark or |x| > pi or cos(lat_eq) cos(x) <= -sin(lat_eq) tan(d).
-  // Within the fp32 error margins the fp64 reference form decides.
-  {
-    const float dv = fmaf(g.sl, u.tan_d_f, cwl);
-    const float ax = fabsf(u.omega_th_f + g.dlon);
-    const float mpi = ax - 3.14159265358979f;
-    bool dark;
-    if (!(fabsf(dv) >= 1e-5f) || !(fabsf(mpi) >= 1e-4f)) {
-      dark = dark_exact(p, geo_d, n_pad, cell, up);
-    } else {
-      dark = (u.flat_dark != 0) || (mpi > 0.0f) || (dv <= 0.0f);
+  // clear-sky shortwave (SF:904-941), only while the sun is up on a flat
+  // surface somewhere this step (flat_dark, a step uniform, makes every cell
+  // dark: K_cs = 0 in the reference too): half the steps skip W_p, tau and
+  // gam_s and the slope geometry
+  float K_cs = 0.0f;
+  if (!u.flat_dark) {
+    const float w = fexp2((0.0614f * kLog2e) * T_dew);
+    const float tau = nmin<NS>(nmax<NS>(fexp2(fmaf(u.tau_c1, w, u.tau_c0)) - p.f_dust, 0.0f), 1.0f);  // SF:614
+    const float gam_s = p.f_1pdust - fexp2(fmaf(u.gam_c1, w, u.gam_c0));
+    // cos(lat_eq)*cos(omega*th + dlon)
+    const float cwl = u.cos_wth_f * g.cc - u.sin_wth_f * g.cs;
+    // SF:887; the geometry planes are never NaN (derive_geo maps a NaN slope or
+    // aspect to the reference's 0), so IEEE max is exact here in both forms
+    const float K_ET = fmaxf(fmaf(u.kc_f, cwl, u.ks_f * g.sl), 0.0f);
+    const float kf = u.k_et_flat_f;
+    const float K_dif = 0.5f * gam_s * kf;
+    const float K_bs = 0.5f * gam_s * albedo * fmaf(tau, kf, K_dif);
+    K_cs = tau * K_ET + K_dif + K_bs;
+    // dark (SF:939-941): with x = omega*th + dlon and ac = acos(clip(-tan(lat_eq) tan(d))),
+    // th <= T_sr or th >= T_ss  <=>  flat_dark or |x| >= ac
+    //                           <=>  flat_dark or |x| > pi or cos(lat_eq) cos(x) <= -sin(lat_eq) tan(d).
+    // Within the fp32 error margins the fp64 reference form decides.
+    {
+      const float dv = fmaf(g.sl, u.tan_d_f, cwl);
+      const float ax = fabsf(u.omega_th_f + g.dlon);
+      const float mpi = ax - 3.14159265358979f;
+      bool dark;
+      if (!(fabsf(dv) >= 1e-5f) || !(fabsf(mpi) >= 1e-4f)) {
+        dark = dark_exact(p, geo_d, n_pad, cell, up);
+      } else {
+        dark = (mpi > 0.0f) || (dv <= 0.0f);  // flat_dark: handled above
+      }
+      if (dark) K_cs = 0.0f;
     }
-    if (dark) K_cs = 0.0f;
   }
   const float Qn_SW = K_cs * (1.0f - albedo);
   // longwave (:1167-1248): em_air - 1 (the balance below needs only that)
