@@ -32,7 +32,7 @@ EXP, EXP_LIBM, LOG, LOG_LIBM, DIV_61121, DIV_3600, EXP_VGPR, FDIV_BY_73, FDIV_73
 
 # the bounds HISTORY.md section 5 states (ulps of numpy's result)
 EXP_ULPS = 3.0  # degree-10 polynomial since round 5 (the device libm's degree 12: 1 ulp)
-LOG_ULPS = 1.0
+LOG_ULPS = 4.0  # absolute, in ulps of max(|log x|, 1): the fp32 seed refined by one exp step (round 5)
 
 
 @pytest.fixture(scope="module")
@@ -145,18 +145,23 @@ def test_exp_within_three_ulp_of_numpy(host):
         assert _same(ev(SPECIAL[[2, 3, 4, 0, 1, 11, 10]], EXP), np.exp(SPECIAL[[2, 3, 4, 0, 1, 11, 10]]))
 
 
-def test_log_within_one_ulp_of_numpy(host):
+def _log_err(got, ref):
+    """|got - ref| in ulps of max(|ref|, 1): log_k's error is absolute (~1e-15), not relative near log x = 0."""
+    return np.abs(got - ref) / np.spacing(np.maximum(np.abs(ref), 1.0))
+
+
+def test_log_within_four_absolute_ulp_of_numpy(host):
     ev, _ = host
     rng = np.random.default_rng(13)
     worst = {}
     for name, x in zip(("physics", "positive range"), log_arguments(rng)):
-        ref = np.log(x)
-        ok = ref != 0
-        worst[name] = float(_ulps(ev(x, LOG)[ok], ref[ok]).max())
-        assert np.all(ev(x, LOG)[~ok] == 0.0)
+        worst[name] = float(_log_err(ev(x, LOG), np.log(x)).max())
     assert max(worst.values()) <= LOG_ULPS, worst
     with np.errstate(divide="ignore", invalid="ignore"):
-        assert _same(ev(SPECIAL, LOG), np.log(SPECIAL))
+        want = np.log(SPECIAL)
+        fin = np.isfinite(want) & (SPECIAL != 1.0)
+        assert _same(ev(SPECIAL, LOG)[~fin], want[~fin])  # 0, -0, inf, -inf, NaN, negatives, log(1) = 0
+        assert _log_err(ev(SPECIAL, LOG)[fin], want[fin]).max() <= LOG_ULPS
 
 
 def _device(x, which):
@@ -171,9 +176,9 @@ def _device(x, which):
 
 @pytest.mark.gpu
 def test_fastmath_on_the_device(host):
-    """The device computes what the host build computes, bit for bit; its exp_k
-    (its constants in scalar registers; exp_kv, the same in vector registers) is within
-    3 ulp of the device libm's exp; its log_k is within 1 ulp of the device libm's log."""
+    """The device computes what the host build computes (bit for bit but for log_k, whose fp32
+    seed differs); its exp_k (constants in scalar registers; exp_kv, in vector registers) is
+    within 3 ulp of the device libm's exp; its log_k within 4 absolute ulp of the libm's log."""
     ev, _ = host
     rng = np.random.default_rng(14)
     xe = np.concatenate([*exp_arguments(rng), SPECIAL])
@@ -183,11 +188,13 @@ def test_fastmath_on_the_device(host):
     assert _ulps(got[fin], libm[fin]).max() <= EXP_ULPS and _same(got[~fin], libm[~fin])
     assert _same(_device(xe, EXP_VGPR), _device(xe, EXP))
     xl = np.concatenate([*log_arguments(rng), SPECIAL])
-    got = _device(xl, LOG)
-    assert _same(got, ev(xl, LOG))
+    got = _device(xl, LOG)  # the device's seed (v_log_f32) differs from the host build's (log2f)
+    host_ = ev(xl, LOG)
+    fin = np.isfinite(host_)
+    assert _log_err(got[fin], host_[fin]).max() <= LOG_ULPS and _same(got[~fin], host_[~fin])
     libm = _device(xl, LOG_LIBM)
-    ok = np.isfinite(libm) & (libm != 0)
-    assert _ulps(got[ok], libm[ok]).max() <= LOG_ULPS and _same(got[~ok], libm[~ok])
+    ok = np.isfinite(libm)
+    assert _log_err(got[ok], libm[ok]).max() <= LOG_ULPS and _same(got[~ok], libm[~ok])
     xd = np.concatenate([_wide(rng, 400_000, -60, 60), SPECIAL])
     for which, c in ((DIV_61121, 6.1121), (DIV_3600, 3600.0)):
         with np.errstate(invalid="ignore"):

@@ -4,13 +4,11 @@
 // this file); per step it evaluates eight exp, three log and about fifteen
 // divisions by a model constant.
 //
-//   log_k(x)       fdlibm's log (k ln2 + log1p(f) with s = f/(2+f) and a
-//                  degree-14 polynomial in s), the division by a two-step
-//                  Newton reciprocal, the polynomials by FMA.  Within 1 ulp of
-//                  numpy's log (measured: tests/test_fastmath.py; 1.7 % of the
-//                  physics' arguments differ by one ulp) where the device
-//                  libm's double-double log is ~100 VALU instructions; this is
-//                  ~40.
+//   log_k(x)       an fp32 seed refined by one step on exp_k (round 5): within
+//                  ~1e-15 absolute of numpy's log, ~27 VALU; fdlibm's log
+//                  (log_fd: k ln2 + log1p(f), s = f/(2+f), degree-14
+//                  polynomial, 1 ulp, ~40 VALU; the device libm's double-double
+//                  log is ~100) for the rare arguments outside [2^-120, 2^120].
 //   div_k(x, c, rc)  x / c for a constant c with rc = RN(1/c) known up front:
 //                  q = RN(x rc), then one FMA correction step, which gives the
 //                  correctly rounded quotient, IEEE division's result bit for
@@ -181,7 +179,7 @@ TFG_FM_HD inline double rcp_approx(double d) {
 #endif
 }
 
-TFG_FM_HD inline double log_k(double x) {
+TFG_FM_HD inline double log_fd(double x) {
   TFG_FM_NO_CONTRACT
 #if defined(__HIP_DEVICE_COMPILE__)
   double m = __builtin_amdgcn_frexp_mant(x);  // [0.5, 1) for finite nonzero x
@@ -233,6 +231,31 @@ TFG_FM_HD inline double div_k(double x, double c, double rc) {
   const double e = fma_vv(-q, c, x);
   const double q1 = fma_vv(e, rc, q);
   return (e < 0.0 || e > 0.0) ? q1 : q;
+}
+
+// ---------------------------------------------------------------------------
+// log (round 5, sized for ~1e-15 absolute): an fp32 seed y0 (v_log_f32, ~1e-7)
+// refined by one step on exp, y = y0 + log1p(x e^-y0 - 1) with log1p(d) = d -
+// d^2/2 (|d| ~ 1e-6, so the cubic term is below 1e-18): one exp_k instead of
+// fdlibm's reduction and degree-14 polynomial.  Its error is exp_k's, ~1e-15
+// absolute; relative near log x = 0 that is looser than fdlibm's 1 ulp
+// (tests/test_fastmath.py bounds it absolutely).  Outside [2^-120, 2^120]
+// (0, denormals, huge, negative, inf, NaN: rare) fdlibm's log_fd.
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double log_k(double x) {
+  TFG_FM_NO_CONTRACT
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y0 = (double)__builtin_amdgcn_logf((float)x) * 0.69314718055994531;
+#else
+  const double y0 = (double)std::log2((float)x) * 0.69314718055994531;
+#endif
+  const double d = fma_vv(x, exp_k(-y0), -1.0);
+  double y = y0 + fma_vv(-0.5 * d, d, d);
+  if (__builtin_expect(!(x >= 0x1p-120 && x < 0x1p120), 0)) {
+    TFG_FM_RARE();
+    y = log_fd(x);
+  }
+  return y;
 }
 
 // x / c for a constant c as x * RN(1/c): within 1 ulp of the quotient, 1 VALU.
