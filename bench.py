@@ -1052,8 +1052,8 @@ def main(args=None):
                 "kernel_ms_per_launch": float(launch_ms.mean()),
                 "bytes_model": dict(zip(("per_step", "per_launch"), bytes_model(elem, args.catchments > 0, args.conduction))),
                 "note": None if args.engine == "float32" else (
-                    "the fp64 engine is issue-bound, not HBM-bound: its step issues 1088-1092 VALU instructions per "
-                    "wave and cell-step (profiles/r3az_issue_counters.json); frac is its HBM share only"),
+                    "the fp64 engine is issue-bound, not HBM-bound: its step issues ~680 VALU instructions per "
+                    "wave and cell-step (profiles/r5_issue_counters.json); frac is its HBM share only"),
             },
             "cpu_baseline": cpu,
             "cpu_baseline_numpy_1core": numpy_leg if world == 1 else None,

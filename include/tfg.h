@@ -293,13 +293,14 @@ int tfg_set_step_form(tfg_handle* h, int form);
 
 /* Self-test of the fp64 engine's power rewrites on the device (tests only):
  * out[i] = pow4(x[i]) (which = 0: T^4, :1231-1233), pow1p5(x[i]) (1: RH^1.5,
- * :1520) or exp(log(x[i]) / 7) (2: em_air's 1/7 power, :1167), computed by the
+ * :1520) or root7(x[i]) (2: em_air's 1/7 power, :1167), computed by the
  * same device functions the engine's steps call; and the fp64 engine's exp,
  * log and constant-divisor division (csrc/tfg_fastmath.hpp): exp_k (3), the
  * device libm's exp (4), log_k (5), the device libm's log (6), x / 6.1121 (7)
  * and x / 3600 (8) by div_k, exp_kv (9: exp_k with its constants in
- * vector registers), fdiv(x, 7.3) (10) and fdiv(7.3, x) (11).  Host arrays of
- * n values, synchronous. */
+ * vector registers), fdiv(x, 7.3) (10), fdiv(7.3, x) (11), and the wet bulb's
+ * arctangent atan_q: atan(x / 7.3) (12) and atan(-7.3 / x) (13).  Host arrays
+ * of n values, synchronous. */
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out);
 
 /* Device-side synthetic workload generator (bench / tests): fills the forcing

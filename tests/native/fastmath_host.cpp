@@ -14,6 +14,8 @@ extern "C" void fm_eval(const double* x, double* y, long n, int which) {
       case 8: y[i] = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
       case 10: y[i] = tfg_fm::fdiv(v, 7.3); break;
       case 11: y[i] = tfg_fm::fdiv(7.3, v); break;
+      case 12: y[i] = tfg_fm::atan_q(v, 7.3); break;
+      case 13: y[i] = tfg_fm::atan_q(-7.3, v); break;
       default: y[i] = 0.0; break;
     }
   }
@@ -27,4 +29,9 @@ extern "C" void fm_div(const double* x, const double* c, double* y, long n) {
 // fdiv(x[i], c[i]): the variable-divisor quotient
 extern "C" void fm_fdiv(const double* x, const double* c, double* y, long n) {
   for (long i = 0; i < n; ++i) y[i] = tfg_fm::fdiv(x[i], c[i]);
+}
+
+// atan_q(x[i], c[i]): atan(x / c) from the two operands
+extern "C" void fm_atan_q(const double* x, const double* c, double* y, long n) {
+  for (long i = 0; i < n; ++i) y[i] = tfg_fm::atan_q(x[i], c[i]);
 }

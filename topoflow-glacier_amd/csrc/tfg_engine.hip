@@ -583,6 +583,8 @@ __global__ void k_selftest_powers(const double* __restrict__ x, double* __restri
       case 9: r = tfg_fm::exp_kv(v); break;
       case 10: r = tfg_fm::fdiv(v, 7.3); break;
       case 11: r = tfg_fm::fdiv(7.3, v); break;
+      case 12: r = tfg_fm::atan_q(v, 7.3); break;
+      case 13: r = tfg_fm::atan_q(-7.3, v); break;
       default: r = tfg_fm::div_k(v, 3600.0, 1.0 / 3600.0); break;
     }
     y[i] = r;
@@ -805,8 +807,8 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.rho_air_Lv = q.rho_air * q.Lv;
   p.rho_H2O_Lf = q.rho_H2O * q.Lf;
   p.inv_rho_H2O_Lf = 1.0 / p.rho_H2O_Lf;
-  p.lhc = q.latent_heat_constant;
-  p.sea_p0 = q.sea_level_p0;
+  p.lhc_100_p0 = q.latent_heat_constant * 100.0 / q.sea_level_p0;
+  p.inv_6p11 = 1.0 / (0.611 * 10.0);
   p.negM_g = -q.M_mass_air * q.g;
   p.R = q.uni_gas_const;
   p.eps = q.eps;
@@ -1598,7 +1600,7 @@ int tfg_reset_diag(tfg_handle* h) {
 }
 
 int tfg_selftest_powers(int device, const double* x, int64_t n, int which, double* out) {
-  if (!x || !out || n < 0 || which < 0 || which > 11) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
+  if (!x || !out || n < 0 || which < 0 || which > 13) return fail(nullptr, TFG_ERR_ARG, "bad arguments");
   if (n == 0) return TFG_OK;
   HIPCHK(nullptr, hipSetDevice(device));
   double* d = nullptr;

@@ -20,12 +20,17 @@
 //                  the same overflow/underflow selects, here behind one test of
 //                  |x|) with a degree-10 polynomial where the libm's is degree
 //                  12: within 3 ulp of numpy's (round 5), and the host build
-//                  below computes exactly what the device does.
+//                  below computes exactly what the device does.  Degree 9
+//                  (1.7e-14, scripts/fit_exp.py) flips a melt gate of the fp64
+//                  dark-test run against the oracle (round 5, not taken).
 //   div_r(x, rc)   x / c as x * RN(1/c), within 1 ulp: every constant divisor
 //                  whose last bit no melt-out gate reads (round 5).
 //   fdiv(x, y)     x / y for a variable y: reciprocal, one Newton step, one
 //                  correction of the quotient (within 1 ulp; round 5: one
 //                  Newton step fewer than IEEE-exactness needs, +3.1 %).
+//   atan_q(n, d)   atan(n / d) from the two operands: octant reduction, one
+//                  fdiv, degree-9 polynomial in x^2 (within 2 ulp; round 5,
+//                  the wet bulb's arctangent).
 //
 // Same-box A/B at 4096^2 (scripts/gpu_ab_f64.sh, profiles/r3f_ab_f64.log):
 // 26.6 -> 31.2 G cell-updates/s (+17 %).  Holding exp's polynomial
@@ -284,6 +289,42 @@ TFG_FM_HD inline double fdiv(double x, double y) {
   r = fma_vv(fma_vv(-y, r, 1.0), r, r);
   const double q = x * r;
   return fma_vv(fma_vv(-q, y, x), r, q);
+}
+
+// ---------------------------------------------------------------------------
+// atan(n / d) from the two operands, with one quotient (round 5; the wet
+// bulb's atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))): the octant of
+// |n / d| picks x = a / b, (a - b) / (a + b) or -b / a (a = |n|, b = |d|), so
+// |x| <= tan(pi/8) and atan(|n / d|) = off + atan(x), off = 0, pi/4 or pi/2
+// (hi + lo); atan(x) = x + x z Q(z), z = x^2, Q of degree 9 fitted by
+// scripts/fit_atan.py (6.8e-17 before rounding).  Within 2 ulp of numpy's
+// arctan(n / d) (tests/test_fastmath.py); d = 0 gives +-pi/2, n = d = 0 NaN.
+// The device libm's atan(u) takes an IEEE division 1 / |u| and a degree-19
+// polynomial on top of the quotient u.
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double atan_q(double n, double d) {
+  TFG_FM_NO_CONTRACT
+  const double a = std::fabs(n), b = std::fabs(d);
+  const bool lo = a <= 0x1.a827999fcef32p-2 * b;  // tan(pi/8)
+  const bool hi = a > 0x1.3504f333f9de6p+1 * b;   // tan(3 pi/8)
+  const double num = lo ? a : (hi ? -b : a - b);
+  const double den = lo ? b : (hi ? a : a + b);
+  const double x = fdiv(num, den);
+  const double z = x * x;
+  double q = fma_vvs(z, 0x1.624ab16a6dac3p-6, -0x1.67e25b96c8da4p-5);
+  q = fma_vvs(z, q, 0x1.d370891418ab2p-5);
+  q = fma_vvs(z, q, -0x1.10245f5158aa3p-4);
+  q = fma_vvs(z, q, 0x1.3b005b34c39e4p-4);
+  q = fma_vvs(z, q, -0x1.745c1a89d2fd5p-4);
+  q = fma_vvs(z, q, 0x1.c71c6a2c4a0ecp-4);
+  q = fma_vvs(z, q, -0x1.249249155d429p-3);
+  q = fma_vvs(z, q, 0x1.999999998297dp-3);
+  q = fma_vvs(z, q, -0x1.5555555555555p-2);
+  const double r = fma_vv(x * z, q, x);
+  const double off_hi = lo ? 0.0 : (hi ? 0x1.921fb54442d18p+0 : 0x1.921fb54442d18p-1);
+  const double off_lo = lo ? 0.0 : (hi ? 0x1.1a62633145c07p-54 : 0x1.1a62633145c07p-55);
+  const double t = off_hi + (r + off_lo);
+  return (std::signbit(n) != std::signbit(d)) ? -t : t;
 }
 
 }  // namespace tfg_fm

@@ -29,6 +29,7 @@ using tfg_fm::div_r;
 using tfg_fm::fdiv;
 using tfg_fm::exp_k;
 using tfg_fm::log_k;
+using tfg_fm::atan_q;
 
 // Earth_Angular_Velocity() (SF:252) [rad/h] and its correctly rounded
 // reciprocal (the divisor of the sunrise/sunset offsets, SF:783-830).
@@ -45,8 +46,8 @@ struct DevParams {
   double rho_air_Cp_air;      // (rho_air*Cp_air)                 :745
   double rho_air_Lv;          // rho_air*Lv                        :932
   double rho_H2O_Lf;          // (rho_H2O*Lf)                      :1368
-  double lhc;                 // latent_heat_constant              :931
-  double sea_p0, negM_g, R;   // -M*g, R_star                      :552
+  double lhc_100_p0;          // lhc*100/sea_p0: lhc/p0 = lhc_100_p0*exp(-x_p0)   :551-556, :931
+  double inv_6p11, negM_g, R; // RN(1/(0.611*10)): RH = e_air*exp(-x_es)*inv_6p11 (:788-802, :838); -M*g, R_star  :552
   double eps, one_minus_eps;  // :817
   double gz;                  // g*z (z = 10 m)                    :640
   double z, kappa, z0;        // :670
@@ -358,70 +359,82 @@ __device__ __forceinline__ double pow4(double x) {
   const double x2 = x * x;
   return x2 * x2;
 }
+// The square root from v_rsq_f64's seed y: s = x y, h = y / 2, one Goldschmidt
+// step and one correction s + (x - s^2) h (round 5; the device libm's sqrt adds
+// range scaling and a second correction): within 1 ulp for x in [2^-900,
+// 2^900]; other x (0, denormals, negatives, inf, NaN) take the libm's.
+__device__ __forceinline__ double sqrt_k(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double s = x * y, h = 0.5 * y;
+  const double r = __builtin_fma(-h, s, 0.5);
+  s = __builtin_fma(s, r, s);
+  h = __builtin_fma(h, r, h);
+  s = __builtin_fma(__builtin_fma(-s, s, x), h, s);
+  if (__builtin_expect(!(x >= 0x1p-900 && x <= 0x1p900), 0)) {
+    TFG_FM_RARE();
+    s = __builtin_sqrt(x);
+  }
+  return s;
+}
 __device__ __forceinline__ double pow1p5(double x) {
 #pragma clang fp contract(off)
-  return x * __builtin_sqrt(x);
+  return x * sqrt_k(x);
 }
-// em_air's (e/T)^(1/7) (:1167): an fp32 seed exp2(log2(x)/7) (relative error
-// ~2e-7) and two Newton steps y <- (6 y + x / y^6) / 7 (error 3 e^2 each, so
-// ~1e-13 then rounding), the reciprocal from v_rcp_f64 and two Newton steps:
+// em_air's (e/T)^(1/7) (:1167): an fp32 seed y0 = exp2(log2(x)/7) (relative
+// error e ~ 2e-7) and one Halley step y0 - y0 (y0^7 - x) / (4 y0^7 + 3 x)
+// (error ~e^3; y0^7 - x is exact, so the step adds only its own roundings):
 // within 2 ulp of numpy's x ** (1/7) (tests/test_power_rewrites.py), at about
-// half the cost of a log and an exp (round 5; before: exp(log(x)/7)).  x = 0
-// gives 0, a negative or NaN x NaN and +inf +inf, as numpy's power.
-__device__ __forceinline__ double rcp_nr(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-  return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-}
+// a third of the cost of a log and an exp (round 5; before: exp(log(x)/7), then
+// two Newton steps).  x = 0 gives 0, a negative or NaN x NaN and +inf +inf, as
+// numpy's power.
 __device__ __forceinline__ double root7(double x) {
 #pragma clang fp contract(off)
   const double y0 = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf((float)x) * (1.0f / 7.0f));
-  double y = y0;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const double y2 = y * y;
-    const double y6 = (y2 * y2) * y2;
-    y = __builtin_fma(y, 6.0 / 7.0, (x * rcp_nr(y6)) * (1.0 / 7.0));
-  }
+  const double y2 = y0 * y0;
+  const double y7 = (y2 * y2) * (y2 * y0);
+  const double c = fdiv(y7 - x, __builtin_fma(4.0, y7, 3.0 * x));
+  const double y = __builtin_fma(-y0, c, y0);
   return (x > 0.0 && x < INFINITY) ? y : y0;
 }
 
 // Stull's wet bulb (:1514-1520, RH a fraction), fp64, with one arctangent for
 // four (round 5; ~1e-14 from the reference's form, tests/test_gpu_parity.py):
 //   atan(T + RH) - atan(RH - 1.676331) = atan((T + 1.676331) / (1 + (T + RH)(RH - 1.676331)))
-//       (+ pi sign(T + RH) where the denominator is negative),
+//       (+ pi sign(T + RH) where the denominator is negative), by atan_q from
+//       the two operands (one quotient),
 //   atan(0.151977 sqrt(RH + 8.313659)) by stull_atan0_poly, and
 //   atan(0.023101 RH) by its series to x^9 (relative error x^10/11 < 1e-10 for
 //       RH <= 5, on a term below 1e-3 K);
 // waves with a lane whose RH is outside [0, 5] take the arctangents there.
-// wet_bulb_parts gives the two arctangent arguments; wet_bulb_finish the rest
-// from their arctangents (the one-cell step batches the arctangents).
+// wet_bulb_parts gives the first arctangent's argument (off the fit) and the
+// second's two operands; wet_bulb_finish the rest from the arctangents (the
+// one-cell step batches the off-fit ones).
 constexpr double kPi = 3.141592653589793;
-__device__ __forceinline__ void wet_bulb_parts(double T_air, double RH, double& u0, double& u1, double& den) {
+__device__ __forceinline__ void wet_bulb_parts(double T_air, double RH, double& u0, double& num, double& den) {
 #pragma clang fp contract(off)
   u0 = 0.151977 * sqrt(RH + 8.313659);
   den = 1.0 + (T_air + RH) * (RH - 1.676331);
-  u1 = fdiv(T_air + 1.676331, den);
+  num = T_air + 1.676331;
 }
 // atan(0.151977 sqrt(RH + 8.313659)) for RH in [0, 5] as a degree-13
 // polynomial in t = 0.4 RH - 1 (a Chebyshev fit, relative error < 2e-14,
-// tests/test_power_rewrites.py): 13 FMAs for a square root and an arctangent.
+// tests/test_power_rewrites.py): 13 FMAs for a square root and an arctangent,
+// the coefficients as scalar operands.
 __device__ __forceinline__ double stull_atan0_poly(double RH) {
   const double t = __builtin_fma(0.4, RH, -1.0);
-  double y = 0x1.b58d687bb4412p-36;
-  y = __builtin_fma(y, t, -0x1.a2f6161678e01p-34);
-  y = __builtin_fma(y, t, 0x1.acccbc15e0e7fp-32);
-  y = __builtin_fma(y, t, -0x1.17d5b0c2a427ap-29);
-  y = __builtin_fma(y, t, 0x1.686a49a337c49p-27);
-  y = __builtin_fma(y, t, -0x1.d44af1ebe2f10p-25);
-  y = __builtin_fma(y, t, 0x1.38df9b2403c64p-22);
-  y = __builtin_fma(y, t, -0x1.b16bbee999fe5p-20);
-  y = __builtin_fma(y, t, 0x1.3be2008d543e9p-17);
-  y = __builtin_fma(y, t, -0x1.f1959460701e0p-15);
-  y = __builtin_fma(y, t, 0x1.bc9c3023533e3p-12);
-  y = __builtin_fma(y, t, -0x1.ea2542f0a20c4p-9);
-  y = __builtin_fma(y, t, 0x1.7aac28df5f664p-5);
-  return __builtin_fma(y, t, 0x1.da94c1a0c29f5p-2);
+  double y = tfg_fm::fma_vvs(t, 0x1.b58d687bb4412p-36, -0x1.a2f6161678e01p-34);
+  y = tfg_fm::fma_vvs(y, t, 0x1.acccbc15e0e7fp-32);
+  y = tfg_fm::fma_vvs(y, t, -0x1.17d5b0c2a427ap-29);
+  y = tfg_fm::fma_vvs(y, t, 0x1.686a49a337c49p-27);
+  y = tfg_fm::fma_vvs(y, t, -0x1.d44af1ebe2f10p-25);
+  y = tfg_fm::fma_vvs(y, t, 0x1.38df9b2403c64p-22);
+  y = tfg_fm::fma_vvs(y, t, -0x1.b16bbee999fe5p-20);
+  y = tfg_fm::fma_vvs(y, t, 0x1.3be2008d543e9p-17);
+  y = tfg_fm::fma_vvs(y, t, -0x1.f1959460701e0p-15);
+  y = tfg_fm::fma_vvs(y, t, 0x1.bc9c3023533e3p-12);
+  y = tfg_fm::fma_vvs(y, t, -0x1.ea2542f0a20c4p-9);
+  y = tfg_fm::fma_vvs(y, t, 0x1.7aac28df5f664p-5);
+  return tfg_fm::fma_vvs(y, t, 0x1.da94c1a0c29f5p-2);
 }
 // RH outside the fits' range [0, 5] (NaN stays on the fits and gives NaN)
 __device__ __forceinline__ bool stull_off_fit(double RH) { return (RH < 0.0) || (RH > 5.0); }
@@ -458,11 +471,11 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
 #pragma clang fp contract(off)
   const double dt = p.dt;
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
-  // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556
+  // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556, read only
+  // as lhc / p0 (:931): (100 lhc / sea_p0) exp(-x), one exp and no quotient
+  // (round 5; within 2 ulp of the reference's quotient)
   const double T_K = T_air + 273.15;
-  double p0 = p.sea_p0 * exp_k(fdiv(p.negM_g * s.elev, p.R * T_K));
-  p0 = div_r(p0, 1.0 / 1000.0);
-  p0 = p0 * 10.0;
+  const double lhc_p0 = p.lhc_100_p0 * exp_k(-fdiv(p.negM_g * s.elev, p.R * T_K));
   // :567, :576, :585, :604, :613, :623
   const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
   const double P_snow = P * ((T_air <= p.T_rs) ? 1.0 : 0.0);
@@ -472,19 +485,19 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     d.PR += P_rain * p.da_m2 * dt;
     d.PS += P_snow * p.da_m2 * dt;
   }
-  // saturation vapour pressure (air) :788-802
-  double e_sat_air;
-  if (!p.satterlund) {
-    e_sat_air = 0.611 * exp_k(fdiv(17.3 * T_air, T_air + 237.3));
-  } else {
-    e_sat_air = div_r(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1.0 / 1000.0);
-  }
-  e_sat_air = e_sat_air * 10.0;
   // :817-826
   double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
   e = div_r(e, 1.0 / 1000.0);
   const double e_air = e * 10.0;
-  const double RH = fdiv(e_air, e_sat_air);  // :838
+  // saturation vapour pressure (air) :788-802, read only as RH = e_air / e_sat_air
+  // (:838): Brutsaert's e_air exp(-x) / 6.11 without the quotient (round 5)
+  double RH;
+  if (!p.satterlund) {
+    RH = (e_air * exp_k(-fdiv(17.3 * T_air, T_air + 237.3))) * p.inv_6p11;
+  } else {
+    const double e_sat_air = div_r(pow(opaque(10.0), 11.4 - fdiv(2353.0, T_air + 273.15)), 1.0 / 1000.0) * 10.0;
+    RH = fdiv(e_air, e_sat_air);
+  }
   // :888-893
   const double log_term = log_k(div_r(e_air, 1.0 / 6.1121));
   const double T_dew = fdiv(257.14 * log_term, 18.678 - log_term);
@@ -511,7 +524,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // :853 (SURFACE uses the air RH)
   const double e_surf = RH * e_sat_surf;
   // :931-934
-  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * fdiv(p.lhc, p0);
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * lhc_p0;
   // albedo :1023-1059 with the fixed-point window
   q_new = window_q(P_snow * dt * p.ws, p.qscale);
   st.tot_q += window_tot(q_new) - window_tot(q_old);
@@ -561,8 +574,8 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // Stull wet bulb (:1514-1520), only needed where it snows
   double T_wb = 0.0;
   if (P_snow > 0.0) {
-    double u0, u1, den;
-    wet_bulb_parts(T_air, RH, u0, u1, den);
+    double u0, num, den;
+    wet_bulb_parts(T_air, RH, u0, num, den);
     const double x = 0.023101 * RH;
     double at0 = stull_atan0_poly(RH), at_small = atan_small_series(x);
     if (__any(stull_off_fit(RH))) {
@@ -570,7 +583,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
       at0 = off ? atan(u0) : at0;
       at_small = off ? atan(x) : at_small;
     }
-    T_wb = wet_bulb_finish(T_air, RH, at0, atan(u1), den, at_small);
+    T_wb = wet_bulb_finish(T_air, RH, at0, atan_q(num, den), den, at_small);
   }
   const DevParams& p4 = params();  // melt and mass phase
   melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
@@ -591,7 +604,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
 // behind one barrier per level; with W = 1 the classes run one after another
 // in the wave and the results are read back from their lanes (v_readlane).
 // The serial chain of fp64 libm calls falls from 14-18 (exp x8, log x3,
-// cos, acos, atan x4 where it snows) to 3 levels.  The same
+// cos, acos, the wet bulb's atan off its fits) to 3 levels.  The same
 // functions on the same arguments give the same values, so the result equals
 // cell_step_exact bit for bit (test_one_cell_kernels_equal_the_grid_kernel).
 // ---------------------------------------------------------------------------
@@ -657,7 +670,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const double x_p0 = fdiv(p.negM_g * s.elev, p.R * T_K);       // :551
     const double x_es = fdiv(17.3 * T_air, T_air + 237.3);        // :788
     const double x_alb = -st.n * r_alb;                          // :1041
-    ex1 = exp_k(lane == 1 ? x_es : (lane == 2 ? x_alb : x_p0));
+    ex1 = exp_k(lane == 1 ? -x_es : (lane == 2 ? x_alb : -x_p0));
   }
   if (X.mine(X_LOG1))  // :670, :888
     lg1 = log_k(lane == 1 ? npmax(div_r(p.z - h_snow, p.inv_z0), 0.01) : div_r(e_air, 1.0 / 6.1121));
@@ -676,14 +689,9 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double pw_ta4 = pow4(T_air_K);  // :1231
   if (W > 1) ac = X.get(X_TRIG1, 0.0, 0);
 
-  // :551-556
-  double p0 = p.sea_p0 * e_p0;
-  p0 = div_r(p0, 1.0 / 1000.0);
-  p0 = p0 * 10.0;
-  // :788-802, :838
-  double e_sat_air = !p.satterlund ? 0.611 * e_es : div_r(pw_es, 1.0 / 1000.0);
-  e_sat_air = e_sat_air * 10.0;
-  const double RH = fdiv(e_air, e_sat_air);
+  // :551-556, :931 (lhc / p0); :788-802, :838 (RH), as cell_step_exact
+  const double lhc_p0 = p.lhc_100_p0 * e_p0;
+  const double RH = !p.satterlund ? (e_air * e_es) * p.inv_6p11 : fdiv(e_air, div_r(pw_es, 1.0 / 1000.0) * 10.0);
   // :888-893, :906-910
   const double T_dew = fdiv(257.14 * log_term, 18.678 - log_term);
   const double T_surf = (h_snow > 0.0 || h_ice > 0.0) ? npmin(T_dew, 0.0) : T_dew;
@@ -718,9 +726,9 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15));  // :796 (surface)
   // Stull wet bulb (:1514-1520), only where it snows: wet_bulb_parts' two arguments and, for RH > 8,
   // the small term's own arctangent
-  double wb_u0 = 0.0, wb_u1 = 0.0, wb_den = 1.0;
-  if (P_snow > 0.0) wet_bulb_parts(T_air, RH, wb_u0, wb_u1, wb_den);
-  if (X.mine(X_ATAN2) && P_snow > 0.0) at2 = atan(lane == 1 ? wb_u1 : (lane == 2 ? 0.023101 * RH : wb_u0));
+  double wb_u0 = 0.0, wb_num = 0.0, wb_den = 1.0;
+  if (P_snow > 0.0) wet_bulb_parts(T_air, RH, wb_u0, wb_num, wb_den);
+  if (X.mine(X_ATAN2) && P_snow > 0.0) at2 = atan(lane == 2 ? 0.023101 * RH : wb_u0);
   X.put(X_EXP2, ex2);
   X.put(X_POW2, pw2);
   X.put(X_ATAN2, at2);
@@ -730,7 +738,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double W_p = 1.12 * X.get(X_EXP2, ex2, 1);
   // :853, :931-934
   const double e_surf = RH * e_sat_surf;
-  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * fdiv(p.lhc, p0);
+  const double Qe = p.rho_air_Lv * Dh * (e_air - e_surf) * lhc_p0;
   const double a_sa = -0.1240 - (0.0207 * W_p);
   const double b_sa = -0.0682 - (0.0248 * W_p);
   const double a_s = -0.0363 - (0.0084 * W_p);
@@ -770,7 +778,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     const bool off = stull_off_fit(RH);
     const double at0 = off ? X.get(X_ATAN2, at2, 0) : stull_atan0_poly(RH);
     const double at_small = off ? X.get(X_ATAN2, at2, 2) : atan_small_series(0.023101 * RH);
-    T_wb = wet_bulb_finish(T_air, RH, at0, X.get(X_ATAN2, at2, 1), wb_den, at_small);
+    T_wb = wet_bulb_finish(T_air, RH, at0, atan_q(wb_num, wb_den), wb_den, at_small);
   }
   melt_and_mass(p, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, true);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
