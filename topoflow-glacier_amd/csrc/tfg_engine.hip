@@ -820,7 +820,7 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.sigma = q.sigma;
   p.em_surf_sigma = q.em_surf * q.sigma;
   p.one_minus_em_surf = 1.0 - q.em_surf;
-  p.one_seventh = 1.0 / 7.0;
+  p.negM_g_R = -q.M_mass_air * q.g / q.uni_gas_const;
   p.T0 = q.T0;
   p.ws = q.rho_H2O / q.rho_snow;
   p.wi = q.rho_H2O / q.rho_ice;

@@ -53,7 +53,7 @@ struct DevParams {
   double z, kappa, z0;        // :670
   double em_surf_sigma, sigma, one_minus_em_surf;
   double inv_rho_H2O_Lf;      // RN(1/(rho_H2O*Lf)): div_k of :1368, :1428
-  double one_seventh;         // np.float64(1)/7                   :292
+  double negM_g_R;            // -M*g/R_star: the pressure exponent's factor    :552
   double T0;                  // T0_cc                             :389
   double Ecci0;               // initial ice cold content          :394-395
   double inv_dt, inv_dt_rhoLf, inv_z0;  // reciprocals (fast variant; inv_dt, inv_z0 also div_k's)
@@ -380,6 +380,29 @@ __device__ __forceinline__ double pow1p5(double x) {
 #pragma clang fp contract(off)
   return x * sqrt_k(x);
 }
+// 1 / d from v_rcp_f64 and two Newton steps (within 1 ulp), or one (rcp_nr1:
+// relative error ~1e-14, for a quotient that only corrects a value).
+__device__ __forceinline__ double rcp_nr1(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+}
+__device__ __forceinline__ double rcp_nr(double d) {
+  const double r = rcp_nr1(d);
+  return __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+}
+
+// The stability correction (:672-726) with one quotient (round 5): Ri = top /
+// bot with bot > 0, so Ri > 0 exactly where top > 0, and Dn / (1 + 10 Ri) =
+// Dn bot / (bot + 10 top), Dn (1 - 10 Ri) = Dn (bot - 10 top) / bot; Ri = 0
+// keeps Dh = Dn exactly.  Within 2 ulp of the reference's two quotients.
+__device__ __forceinline__ double stability_dh(double Dn, double top, double bot) {
+#pragma clang fp contract(off)
+  const bool stable = top > 0.0;
+  const double num = Dn * (stable ? bot : bot - (10.0 * top));
+  const double den = stable ? bot + (10.0 * top) : bot;
+  return (top == 0.0) ? Dn : fdiv(num, den);
+}
+
 // em_air's (e/T)^(1/7) (:1167): an fp32 seed y0 = exp2(log2(x)/7) (relative
 // error e ~ 2e-7) and one Halley step y0 - y0 (y0^7 - x) / (4 y0^7 + 3 x)
 // (error ~e^3; y0^7 - x is exact, so the step adds only its own roundings):
@@ -392,7 +415,7 @@ __device__ __forceinline__ double root7(double x) {
   const double y0 = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf((float)x) * (1.0f / 7.0f));
   const double y2 = y0 * y0;
   const double y7 = (y2 * y2) * (y2 * y0);
-  const double c = fdiv(y7 - x, __builtin_fma(4.0, y7, 3.0 * x));
+  const double c = (y7 - x) * rcp_nr1(__builtin_fma(4.0, y7, 3.0 * x));  // a correction ~e: 1e-14 of it suffices
   const double y = __builtin_fma(-y0, c, y0);
   return (x > 0.0 && x < INFINITY) ? y : y0;
 }
@@ -473,9 +496,11 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double h_snow = st.h_snow, h_ice = st.h_ice;  // previous step
   // update_atm_pressure_from_elevation(T_C=True, MBAR=True) :551-556, read only
   // as lhc / p0 (:931): (100 lhc / sea_p0) exp(-x), one exp and no quotient
-  // (round 5; within 2 ulp of the reference's quotient)
+  // (round 5; within 2 ulp of the reference's quotient); 1 / T_K serves the
+  // exponent and em_air's argument (:1167)
   const double T_K = T_air + 273.15;
-  const double lhc_p0 = p.lhc_100_p0 * exp_k(-fdiv(p.negM_g * s.elev, p.R * T_K));
+  const double r_TK = rcp_nr(T_K);
+  const double lhc_p0 = p.lhc_100_p0 * exp_k(-((p.negM_g_R * s.elev) * r_TK));
   // :567, :576, :585, :604, :613, :623
   const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
   const double P_snow = P * ((T_air <= p.T_rs) ? 1.0 : 0.0);
@@ -514,11 +539,10 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double top = p.gz * (T_air - T_surf);
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
-  const double Ri = fdiv(top, bot);
   // :670-726
   const double arg = fdiv(p.kappa, log_k(npmax(div_r(p.z - h_snow, p.inv_z0), 0.01)));
   const double Dn = uz * (arg * arg);
-  const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  const double Dh = stability_dh(Dn, top, bot);
   // :744-745
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
   // :853 (SURFACE uses the air RH)
@@ -558,7 +582,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   const double T_air_K = T_air + 273.15;
   double em_air;
   if (!p3.satterlund) {
-    const double term1 = p3.one_minus_F_172 * root7(fdiv(div_r(e_air, 1.0 / 10.0), T_air_K));
+    const double term1 = p3.one_minus_F_172 * root7(div_r(e_air, 1.0 / 10.0) * r_TK);
     em_air = (term1 * p3.cloud_term) + p3.F;
   } else {
     em_air = 1.08 * (1.0 - exp_k(-1.0 * pow(e_air, div_r(T_air_K, 1.0 / 2016.0))));
@@ -667,7 +691,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // ---- level 1: arguments from inputs, state, statics and uniforms
   double ex1 = 0.0, lg1 = 0.0, cos_wl = 0.0, ac = 0.0, pw1 = 0.0;
   if (X.mine(X_EXP1)) {
-    const double x_p0 = fdiv(p.negM_g * s.elev, p.R * T_K);       // :551
+    const double x_p0 = (p.negM_g_R * s.elev) * rcp_nr(T_K);      // :551, as cell_step_exact
     const double x_es = fdiv(17.3 * T_air, T_air + 237.3);        // :788
     const double x_alb = -st.n * r_alb;                          // :1041
     ex1 = exp_k(lane == 1 ? -x_es : (lane == 2 ? x_alb : -x_p0));
@@ -699,10 +723,9 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double top = p.gz * (T_air - T_surf);
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
-  const double Ri = fdiv(top, bot);
   const double arg = fdiv(p.kappa, log_dn);
   const double Dn = uz * (arg * arg);
-  const double Dh = (Ri > 0.0) ? fdiv(Dn, 1.0 + (10.0 * Ri)) : Dn * (1.0 - (10.0 * Ri));
+  const double Dh = stability_dh(Dn, top, bot);
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
   // albedo (:1041-1059)
   const double snow_albedo = 0.4 + 0.44 * e_alb;
@@ -762,7 +785,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   // :1167-1192, :1231-1248
   double em_air;
   if (!p.satterlund) {
-    const double term1 = p.one_minus_F_172 * root7(fdiv(div_r(e_air, 1.0 / 10.0), T_air_K));
+    const double term1 = p.one_minus_F_172 * root7(div_r(e_air, 1.0 / 10.0) * rcp_nr(T_air_K));
     em_air = (term1 * p.cloud_term) + p.F;
   } else {
     em_air = 1.08 * (1.0 - X.get(X_EXP2, ex2, 2));
