@@ -52,3 +52,41 @@ def test_n4_rank0_deep_launch_sample(monkeypatch):
     assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
     assert par["max_floored_rel_fp64_baseline"] < 1e-12
     assert np.isfinite(par["max_floored_rel_incl_depletion_rates"])
+
+
+def test_n4_rank2_deep_launch_sample(monkeypatch):
+    """Rank 2 of the same N = 4 line, the rank whose own sample (global rows
+    4096-4103, the bench's default 65 536 cells) has the largest error of any
+    rank of the 2-, 4- and 8-GPU lines (profiles/r5_deep_samples.json,
+    other_ranks: 9.56e-6, at a melt onset): the check the driver's line makes
+    on that rank, held to the 1e-5 tolerance itself."""
+    import torch
+
+    import bench
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+    from topoflow_glacier.synthetic import diurnal_table
+
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--ny", "8192", "--nx", "8192"])
+    args = bench.parse()
+    world, rank = 4, 2
+    plan = bench.shard_plan(args, world, rank)
+    assert (plan["row0"], plan["rows"]) == (4096, 2048)
+    args.fuse = bench.auto_fuse(plan["rows"] * args.nx)
+    assert args.fuse == 384
+    cfg = TopoflowGlacierConfig.model_validate(dict(bench.BASE_CFG, ny=plan["rows"], nx=args.nx, dt=args.dt))
+    eng = GlacierEngine(cfg, plan["rows"], args.nx, engine="float32", device=0, n_frames=args.frames,
+                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=plan["row0"])
+    try:
+        eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
+        cap = bench.capture_parity(eng, args, plan, world, torch, 0)
+    finally:
+        eng.close()
+    assert cap["plan"]["launch_steps"] == [1, 384]
+    par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
+    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
+                               "flips_fp64_baseline", "depletion_steps", "melt_onsets_explained")})
+    assert par["global_rows"] == [4096, 4103]
+    assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
+    assert par["max_floored_rel"] <= 1e-5, par["max_floored_rel_at"]
+    assert par["max_floored_rel_fp64_baseline"] < 1e-12
