@@ -297,8 +297,9 @@ TFG_FM_HD inline double fdiv(double x, double y) {
 // |n / d| picks x = a / b, (a - b) / (a + b) or -b / a (a = |n|, b = |d|), so
 // |x| <= tan(pi/8) and atan(|n / d|) = off + atan(x), off = 0, pi/4 or pi/2
 // (hi + lo); atan(x) = x + x z Q(z), z = x^2, Q of degree 9 fitted by
-// scripts/fit_atan.py (6.8e-17 before rounding).  Within 2 ulp of numpy's
-// arctan(n / d) (tests/test_fastmath.py); d = 0 gives +-pi/2, n = d = 0 NaN.
+// scripts/fit_atan.py (6.8e-17 before rounding).  Within 2 ulp of the
+// arctangent of the exact quotient (tests/test_fastmath.py); d = 0 gives
+// +-pi/2, n = d = 0 NaN.
 // The device libm's atan(u) takes an IEEE division 1 / |u| and a degree-19
 // polynomial on top of the quotient u.
 // ---------------------------------------------------------------------------
