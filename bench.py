@@ -185,6 +185,9 @@ def parse():
     ap.add_argument("--fuse", type=int, default=0,
                     help="steps per launch (= output history slots); 0 = by shard size (auto_fuse)")
     ap.add_argument("--engine", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--flux", default="fp32", choices=["fp32", "fp64"],
+                    help="the float32 engine's flux arithmetic (tfg_set_flux): fp64 = the dew point, turbulent "
+                         "fluxes and long-wave balance in fp64")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default: one --ny x --nx grid row-partitioned over the ranks, BASELINE "
                          "config 4) or weak (--ny rows per rank)")
@@ -432,7 +435,8 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
     # baseline (C oracle vs numpy oracle) and, for the fp32 engine, melt onsets (E_in - Eccs cancelling),
     # classified as the GPU suite does (tests/harness.py classify_sample)
     note("parity: classifying the sample")
-    cls = classify_sample(gpu, ref, c64, cfg, tol, onsets=args.engine == "float32")
+    # the melt-onset allowance is the fp32 flux's only (the fp64-flux form is held without it)
+    cls = classify_sample(gpu, ref, c64, cfg, tol, onsets=args.engine == "float32" and args.flux == "fp32")
     excused, flip, genuine, onset, ok = cls.excused, cls.flip, cls.genuine, cls.onset, cls.ok
     flip64, genuine64, ex64, onset_ok = cls.flip64, cls.genuine64, cls.ex64, cls.onset_ok
     # each output's floor s_v from the whole sample (as the classifiers take it), not the compared part
@@ -476,7 +480,8 @@ def sample_parity(args, plan: dict, world: int, rank: int, threads: int, cap: di
     mass = {"catchments": kc, "cells": plan["rows"] * nx, "vol_P_PR_PS_max_rel": p_err,
             "vol_P_PR_PS_tolerance": 1e-6, "P_max_exact": bool(np.array_equal(diag[:kc, 5], cap["want_P_max"])),
             "vs": "fp64 sums of the forcing frames the shard read (torch on the device), per catchment"}
-    engine_desc = ("k_fused<float, READ_DEPTHS=false, CATCH=%s, QC=false, clean form>" % ("true" if args.catchments else "false")
+    engine_desc = ("k_fused<float, READ_DEPTHS=false, CATCH=%s, QC=false, clean form%s>"
+                   % ("true" if args.catchments else "false", ", fp64 flux" if args.flux == "fp64" else "")
                    if args.engine == "float32" else "k_fused<double, exact, READ_DEPTHS=false>")
     parity = {"vs": "numpy oracle (fp64; pinned bit-exact to the reference fixtures)", "rank": rank,
               "global_rows": [row0, row0 + rows - 1], "cells": n, "steps": pp["launch_steps"][1],
@@ -553,8 +558,9 @@ def pmc_traffic(rows, args):
     null, with the reason."""
     from topoflow_glacier import _native as nat
 
-    suffix = "" if args.engine == "float32" else "_f64"
-    symbol = nat.BENCH_KERNEL if args.engine == "float32" else nat.BENCH_KERNEL_F64
+    suffix = ("_fluxf64" if args.flux == "fp64" else "") if args.engine == "float32" else "_f64"
+    symbol = ((nat.BENCH_KERNEL_PREC if args.flux == "fp64" else nat.BENCH_KERNEL) if args.engine == "float32"
+              else nat.BENCH_KERNEL_F64)
     pmc = ROOT / "profiles" / f"pmc_{args.nx}x{rows}_fuse{args.fuse}{suffix}.json"
     if args.catchments or args.dt != 1.0 or args.conduction:
         return None, {"profile": None, "reason": "no PMC profile for this variant of the kernel"}
@@ -815,12 +821,15 @@ def launch_ranks(args, argv: list[str]) -> int | None:
     return proc.wait()
 
 
-def agree_on_depth(args, pg: bool, torch, dist, local: int, backend: str) -> int:
+def agree_on_depth(depth: int, pg: bool, torch, dist, local: int, backend: str) -> int:
     """Every rank fuses the same depth: the smallest any rank could allocate
-    (a rank whose tfg_create ran out of memory stepped down DEPTH_LADDER)."""
+    (a rank whose tfg_create ran out of memory stepped down DEPTH_LADDER).  A
+    rank that could allocate none joins with 0, so the collective completes on
+    every rank and all of them stop (the caller exits non-zero on 0) instead of
+    the others waiting for it until the process-group timeout."""
     if not pg:
-        return args.fuse
-    t = torch.tensor([args.fuse], dtype=torch.int64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+        return depth
+    t = torch.tensor([depth], dtype=torch.int64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return int(t.item())
 
@@ -869,9 +878,10 @@ def main(args=None):
         if args.fuse != auto:
             depth_note = f"{auto}-step history over the {DEVICE_BYTES_BUDGET / 1e9:.0f} GB budget; fused {args.fuse} steps"
     def create(depth: int):
-        return GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames,
+        return GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames, flux=args.flux,
                              hist_depth=depth, fuse_steps=depth, row0=row0, n_catch=n_catch)
 
+    eng, create_error = None, None
     while True:
         try:
             eng = create(args.fuse)
@@ -881,11 +891,18 @@ def main(args=None):
             # next shallower one (each divides the timed step count)
             smaller = [d for d in DEPTH_LADDER if d < args.fuse]
             if fuse_explicit or not smaller or "memory" not in str(e).lower():
-                raise
+                create_error = e
+                break
             depth_note = f"{args.fuse}-step history did not fit ({e}); fused {smaller[0]} steps"
             args.fuse = smaller[0]
             torch.cuda.empty_cache()
-    agreed = agree_on_depth(args, pg, torch, dist, local, backend)  # one collective, on every rank
+    # one collective on every rank, the failed ones included (they join with 0)
+    agreed = agree_on_depth(0 if eng is None else args.fuse, pg, torch, dist, local, backend)
+    if eng is None:
+        raise create_error
+    if agreed == 0:
+        eng.close()
+        raise SystemExit(f"rank {rank}: another rank could not create its engine at any depth; stopping")
     if agreed != args.fuse:  # another rank stepped down: this one follows, so every rank times the same launches
         eng.close()
         torch.cuda.empty_cache()
@@ -1032,7 +1049,9 @@ def main(args=None):
             "data": "synthetic (counter-hash DEM/forcing with CSV statistics, 24 HBM-resident hourly frames)",
             "config": {
                 "workload": f"{plan['workload']}, {args.dt:g} h steps, "
-                            f"{args.engine} engine (fp64 state), {args.fuse} steps fused per launch"
+                            f"{args.engine} engine (fp64 state"
+                            + (", fp64 flux" if args.engine == "float32" and args.flux == "fp64" else "")
+                            + f"), {args.fuse} steps fused per launch"
                             + (f", {args.catchments} catchments" if args.catchments else "")
                             + (", lateral conduction re-evaluated before every launch" if args.conduction else ""),
                 "grid_per_gpu": [rows, args.nx],

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 6
+#define TFG_ABI_VERSION 7
 
 /* status codes */
 enum {
@@ -290,6 +290,18 @@ int tfg_nan_safe_launches(tfg_handle* h, int64_t* count);
 #define TFG_FORM_AUTO 0
 #define TFG_FORM_NAN_SAFE 1
 int tfg_set_step_form(tfg_handle* h, int form);
+
+/* The fp32 engine's energy-flux precision (ABI 7, round 6): TFG_FLUX_F32 (the
+ * default) computes the step's flux terms in fp32; TFG_FLUX_F64 computes the
+ * dew point (:888-910), the turbulent fluxes (:640-745, :919-934) and the
+ * long-wave balance (:1146-1257) in fp64, so that the cold content Eccs, which
+ * integrates E_in = Q_sum dt over a cold spell (:1496-1564), carries no fp32
+ * rounding into the snow melt at melt onset (:1321-1373).  Forcing, state
+ * layout and outputs are the same; the fp64 engine ignores it.  Replaces no
+ * reference interface (the reference is fp64 numpy throughout). */
+#define TFG_FLUX_F32 0
+#define TFG_FLUX_F64 1
+int tfg_set_flux(tfg_handle* h, int flux);
 
 /* Self-test of the fp64 engine's power rewrites on the device (tests only):
  * out[i] = pow4(x[i]) (which = 0: T^4, :1231-1233), pow1p5(x[i]) (1: RH^1.5,

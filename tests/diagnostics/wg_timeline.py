@@ -70,8 +70,8 @@ def main():
             e.fill_synthetic(20251001, diurnal_table(24), nx_global=nx)
             e.run(k * max(2, 3840 // k))  # warm-up
             e.sync()
-            n_work = -(-e.n // 64) * 64  # k_fused steps the plane stride, skew included (TFG_STEP_SKEW)
-            n_work += 512 if n_work >= 1 << 20 and os.environ.get("TFG_STEP_SKEW", "1") != "0" else 0
+            n_work = -(-e.n // 64) * 64  # k_fused steps the plane stride, skew included
+            n_work += 512 if n_work >= 1 << 20 else 0
             nwg = min(131072, -(-n_work // 256))  # fused_blocks: one workgroup per 256-cell chunk, capped
             runs = []
             for _ in range(3):

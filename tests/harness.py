@@ -346,11 +346,11 @@ def classify_sample(gpu: dict, ref: dict, c64: dict, cfg: dict, tol: float, onse
 
 
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
-                fuse_steps: int = 24, row0: int = 0):
+                fuse_steps: int = 24, row0: int = 0, flux: str = "fp32"):
     from topoflow_glacier.engine import GlacierEngine
 
     return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
-                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0)
+                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0, flux=flux)
 
 
 def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,

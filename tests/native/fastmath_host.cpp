@@ -31,6 +31,11 @@ extern "C" void fm_fdiv(const double* x, const double* c, double* y, long n) {
   for (long i = 0; i < n; ++i) y[i] = tfg_fm::fdiv(x[i], c[i]);
 }
 
+// fdiv_z(x[i], c[i]): fdiv with IEEE's quotient for a zero or infinite operand
+extern "C" void fm_fdiv_z(const double* x, const double* c, double* y, long n) {
+  for (long i = 0; i < n; ++i) y[i] = tfg_fm::fdiv_z(x[i], c[i]);
+}
+
 // atan_q(x[i], c[i]): atan(x / c) from the two operands
 extern "C" void fm_atan_q(const double* x, const double* c, double* y, long n) {
   for (long i = 0; i < n; ++i) y[i] = tfg_fm::atan_q(x[i], c[i]);

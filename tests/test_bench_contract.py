@@ -317,3 +317,36 @@ def test_multi_rank_line_is_self_verifying():
         assert sp["ok"] and sp["global_rows"][0] == x["row0"] and sp["genuine_mismatches"] == 0
         assert sp["steps"] == 24 and sp["launch_steps"] == [1, 24]
     assert d["sample_parity"]["ok"] and d["sample_parity"]["ranks_checked"] == [0, 1]
+
+
+def _agree_worker(rank, world, port, depths, out):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bench, _ = _args()
+    try:
+        out[rank] = bench.agree_on_depth(depths[rank], True, torch, dist, 0, "gloo")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("depths,want", [((384, 256), 256), ((384, 0), 0), ((0, 128), 0)])
+def test_depth_agreement_completes_when_a_rank_cannot_allocate(depths, want):
+    """agree_on_depth: every rank reaches the one all-reduce, a rank
+    that could create no engine joining with 0; all ranks then see the minimum
+    (0: every rank stops with an error instead of waiting for the failed one
+    until the process-group timeout).  gloo, world size 2, on CPU."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = mp.Manager().dict()
+    mp.spawn(_agree_worker, args=(2, port, depths, out), nprocs=2, join=True)
+    assert dict(out) == {0: want, 1: want}

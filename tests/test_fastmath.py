@@ -47,6 +47,7 @@ def host(tmp_path_factory):
     lib.fm_div.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
     lib.fm_fdiv.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
     lib.fm_atan_q.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
+    lib.fm_fdiv_z.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long]
 
     def ev(x, which):
         x = np.ascontiguousarray(x, dtype=np.float64)
@@ -63,6 +64,7 @@ def host(tmp_path_factory):
 
     div.fdiv = lambda x, c: div(x, c, lib.fm_fdiv)
     div.atan_q = lambda x, c: div(x, c, lib.fm_atan_q)
+    div.fdiv_z = lambda x, c: div(x, c, lib.fm_fdiv_z)
     return ev, div
 
 
@@ -134,6 +136,21 @@ def test_variable_division_within_one_ulp(host):
         assert np.isnan(div.fdiv(np.array([a]), np.array([b]))[0])
     assert (div.fdiv(np.array([0.0, -0.0]), np.array([5.0, 5.0])) == 0.0).all()  # (the sign of a zero quotient
     # may differ from IEEE's; no comparison or select of the step reads it)
+
+
+def test_zero_divisor_gives_the_ieee_quotient(host):
+    """fdiv_z (kappa / log((z - h_snow)/z0), :670, whose log is 0 at h_snow = z - z0):
+    fdiv's quotient for finite nonzero operands, IEEE's inf / 0 / NaN for a zero or
+    infinite operand, as the reference's numpy division gives them."""
+    _, div = host
+    rng = np.random.default_rng(17)
+    x, y = _wide(rng, 100_000, -30, 30), _wide(rng, 100_000, -30, 30)
+    assert np.array_equal(div.fdiv_z(x, y), div.fdiv(x, y))
+    a = np.array([0.408, -0.408, 0.408, 0.408, np.inf, 0.0, 0.0, np.nan, 1.0])
+    b = np.array([0.0, 0.0, -0.0, np.inf, 2.0, 0.0, np.inf, 1.0, np.nan])
+    assert np.isnan(div.fdiv(a[:1], b[:1])).all()  # the unguarded form's NaN
+    with np.errstate(divide="ignore", invalid="ignore"):
+        assert _same(div.fdiv_z(a, b), a / b)
 
 
 def test_exp_within_three_ulp_of_numpy(host):

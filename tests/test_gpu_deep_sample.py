@@ -9,6 +9,12 @@ whole shard; bench.sample_parity: the numpy oracle on the same cells, the
 classification of tests/harness.py) on global rows 0-9 -- a superset of the
 rows 0-7 the N = 4 line samples itself -- and holds its max_floored_rel to
 8e-6, the 1e-5 tolerance with a 20 % margin.
+
+Every other BASELINE GPU configuration is checked at ITS timed launch depth
+the same way: config 3 (4096^2, one 384-step launch) and
+config 5's per-GPU slab (rank 3 of 8: rows 6144-8191 of the 16384^2 grid,
+dt = 0.25 h, 43 catchments, one 256-step launch), and rank 2 of the N = 4
+line, whose own sample had the largest error of any rank in round 5.
 """
 import sys
 
@@ -52,6 +58,69 @@ def test_n4_rank0_deep_launch_sample(monkeypatch):
     assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
     assert par["max_floored_rel_fp64_baseline"] < 1e-12
     assert np.isfinite(par["max_floored_rel_incl_depletion_rates"])
+
+
+def _timed_depth_sample(monkeypatch, argv, world, rank, want_fuse, want_rows, flux="fp32"):
+    """bench.capture_parity + sample_parity of one rank of a bench line, on one
+    GPU, at the line's own timed launch depth; returns the parity record."""
+    import torch
+
+    import bench
+    from topoflow_glacier.bmi.config import TopoflowGlacierConfig
+    from topoflow_glacier.engine import GlacierEngine
+    from topoflow_glacier.synthetic import diurnal_table
+
+    monkeypatch.setattr(sys, "argv", ["bench.py", *argv, "--flux", flux])
+    args = bench.parse()
+    plan = bench.shard_plan(args, world, rank)
+    assert (plan["row0"], plan["rows"]) == want_rows
+    args.fuse = bench.auto_fuse(plan["rows_max"] * args.nx)
+    assert args.fuse == want_fuse
+    cfg = TopoflowGlacierConfig.model_validate(dict(bench.BASE_CFG, ny=plan["rows"], nx=args.nx, dt=args.dt))
+    n_catch = args.catchments + 1 if args.catchments > 0 else 1
+    eng = GlacierEngine(cfg, plan["rows"], args.nx, engine="float32", device=0, n_frames=args.frames,
+                        hist_depth=args.fuse, fuse_steps=args.fuse, row0=plan["row0"], n_catch=n_catch, flux=flux)
+    try:
+        eng.fill_synthetic(args.seed, diurnal_table(args.frames), nx_global=args.nx)
+        if args.catchments > 0:
+            eng.set_field("catch_id", bench.catchment_blocks(plan["row0"], plan["rows"], plan["ny_global"], args.nx,
+                                                             args.catchments))
+        cap = bench.capture_parity(eng, args, plan, world, torch, 0)
+    finally:
+        eng.close()
+    assert cap["plan"]["launch_steps"] == [1, want_fuse]
+    par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
+    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
+                               "flips_fp64_baseline", "depletion_steps", "melt_onsets_explained")})
+    assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
+    assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
+    assert par["max_floored_rel_fp64_baseline"] < 1e-12
+    if flux == "fp64":  # held without the melt-onset allowance (bench.sample_parity)
+        assert par["melt_onsets_explained"] == 0
+    return par
+
+
+def test_config3_at_its_timed_depth(monkeypatch):
+    """BASELINE config 3 (4096 x 4096, the bench line's 384-step launches)."""
+    par = _timed_depth_sample(monkeypatch, ["--ny", "4096", "--nx", "4096"], 1, 0, 384, (0, 4096))
+    assert par["global_rows"][0] == 0
+
+
+def test_config5_slab_at_its_timed_depth(monkeypatch):
+    """BASELINE config 5's per-GPU slab: rank 3 of the 8-GPU 16384 x 16384 line
+    (rows 6144-8191), 15-minute steps (a 288-slot window), 43 catchments, the
+    line's 256-step launches; the per-catchment mass balance of the launch is
+    part of the check (bench.sample_parity)."""
+    argv = ["--ny", "16384", "--nx", "16384", "--dt", "0.25", "--catchments", "43"]
+    par = _timed_depth_sample(monkeypatch, argv, 8, 3, 256, (6144, 2048))
+    assert par["global_rows"][0] == 6144
+
+
+@pytest.mark.parametrize("rank,rows", [(0, (0, 2048)), (2, (4096, 2048))])
+def test_n4_deep_launch_with_the_fp64_flux(monkeypatch, rank, rows):
+    """The N = 4 line's rank 0 and rank 2 samples with the fp64-flux form
+    (--flux fp64): 8e-6 and no melt onset explained by the fp32-flux allowance."""
+    _timed_depth_sample(monkeypatch, ["--ny", "8192", "--nx", "8192"], 4, rank, 384, rows, flux="fp64")
 
 
 def test_n4_rank2_deep_launch_sample(monkeypatch):

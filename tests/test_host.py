@@ -186,7 +186,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 17
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.tfg_abi_version() == _native.ABI_VERSION == 6
+    assert L.tfg_abi_version() == _native.ABI_VERSION == 7
     assert b"gfx950" in L.tfg_build_info()
 
 
@@ -320,6 +320,11 @@ def test_create_rejects_oversize_shards_before_touching_the_gpu():
     for bad in ((0, 8, nat.F32, 1, 1, 1), (8, 8, 7, 1, 1, 1), (8, 8, nat.F32, 0, 1, 1), (8, 8, nat.F32, 1, 1, 513)):
         ny, nx, eng, fr, hd, nc = bad
         assert L.tfg_create(ctypes.byref(p), ny, nx, eng, 0, fr, hd, nc, ctypes.byref(h)) == nat.ERR_ARG, bad
+    # z0_air feeds derive_params' log2(z / z0): zero, negative, NaN and inf are refused
+    for z0 in (0.0, -0.001, float("nan"), float("inf")):
+        p.z0_air = z0
+        assert L.tfg_create(ctypes.byref(p), 8, 8, nat.F32, 0, 1, 1, 1, ctypes.byref(h)) == nat.ERR_ARG, z0
+        assert b"z0_air" in L.tfg_last_error(None)
 
 
 def test_ice_flow_entry_points_reject_bad_arguments_without_a_device():

@@ -668,6 +668,7 @@ struct tfg_handle {
   int state_recheck = 0;             // launches before a dirty state is checked again
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
   bool force_ns = false;             // tfg_set_step_form(TFG_FORM_NAN_SAFE): every launch NaN-safe
+  bool flux_f64 = false;             // tfg_set_flux(TFG_FLUX_F64): the fp32 engine's fp64-flux form
   std::string err;
 };
 
@@ -875,6 +876,14 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.f_em_sc = 102.4f;  // 0.1 * 2^10
   p.f_ccFs = (float)(p.one_minus_F_172 * p.cloud_term * std::exp2(-10.0 / 7.0));
   p.f_Fm1 = (float)(q.canopy_factor - 1.0);
+  p.d_eps100 = 100.0 * q.eps;
+  p.d_ome100 = 100.0 * (1.0 - q.eps);
+  p.d_k2 = (q.kappa / std::log(2.0)) * (q.kappa / std::log(2.0));
+  p.d_l2k = (double)p.f_l2k2 * 0.5;
+  p.d_l2kk = (double)p.f_l2kk;
+  p.d_qe = p.rho_air_Lv * q.latent_heat_constant * 100.0 / q.sea_level_p0;
+  p.d_es_k = q.satterlund ? 2353.0 * std::log(10.0) : 17.3 * 237.3;
+  p.d_es_c = q.satterlund ? 273.15 : 237.3;
 }
 
 void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {
@@ -942,6 +951,12 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
     HIPCHK(h, launch_fused_exact(a, fb, rd, ct, h->qc_on, blocks, lds, h->stream));
     return TFG_OK;
   } else {
+  if (h->flux_f64) {  // the fp64-flux form's instantiations live in tfg_fused_prec.hip
+    const FusedBufs fb = {d_u, h->forc, h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->slab,
+                          h->qc};
+    HIPCHK(h, launch_fused_prec(a, fb, rd, ct, h->qc_on, ns, blocks, lds, h->stream));
+    return TFG_OK;
+  }
   constexpr int C = kCellsPerThread;
 #define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, \
                  h->slab, (const R*)h->qc
@@ -1017,6 +1032,9 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   if (n_catch > 512) return fail(nullptr, TFG_ERR_ARG, "n_catch > 512 not supported");
   if (p->ring_len < 1) return fail(nullptr, TFG_ERR_ARG, "ring_len must be >= 1");
   if (!(p->dt > 0)) return fail(nullptr, TFG_ERR_ARG, "dt must be > 0");
+  // derive_params takes log2(z / z0_air) and squares its rounding (the roughness
+  // log's scaling): a z0_air that is zero, negative, NaN or infinite has none
+  if (!(p->z0_air > 0.0 && p->z0_air < INFINITY)) return fail(nullptr, TFG_ERR_ARG, "z0_air must be finite and > 0");
   tfg_handle* h = new (std::nothrow) tfg_handle();
   if (!h) return fail(nullptr, TFG_ERR_ARG, "out of host memory");
   auto bail = [&](int rc) {
@@ -1180,6 +1198,12 @@ int tfg_set_fuse(tfg_handle* h, int k) {
 int tfg_set_step_form(tfg_handle* h, int form) {
   if (!h || (form != TFG_FORM_AUTO && form != TFG_FORM_NAN_SAFE)) return fail(h, TFG_ERR_ARG, "form must be TFG_FORM_AUTO or TFG_FORM_NAN_SAFE");
   h->force_ns = form == TFG_FORM_NAN_SAFE;
+  return TFG_OK;
+}
+
+int tfg_set_flux(tfg_handle* h, int flux) {
+  if (!h || (flux != TFG_FLUX_F32 && flux != TFG_FLUX_F64)) return fail(h, TFG_ERR_ARG, "flux must be TFG_FLUX_F32 or TFG_FLUX_F64");
+  h->flux_f64 = flux == TFG_FLUX_F64;  // the fp64 engine computes every flux in fp64 either way
   return TFG_OK;
 }
 

@@ -281,7 +281,7 @@ TFG_FM_HD inline double div_r(double x, double rc) {
 // equal in > 99.9 %), 6 VALU instead of the 11 of the general sequence
 // (v_div_scale x2, v_rcp, five FMAs, v_div_fmas, v_div_fixup).  For finite x and finite nonzero y (every
 // quotient of the physics); NaN propagates.  A zero or infinite operand gives
-// NaN, where IEEE gives inf or 0: the fp64 step never divides by them.
+// NaN, where IEEE gives inf or 0: fdiv_z below for a divisor that can be zero.
 // ---------------------------------------------------------------------------
 TFG_FM_HD inline double fdiv(double x, double y) {
   TFG_FM_NO_CONTRACT
@@ -289,6 +289,19 @@ TFG_FM_HD inline double fdiv(double x, double y) {
   r = fma_vv(fma_vv(-y, r, 1.0), r, r);
   const double q = x * r;
   return fma_vv(fma_vv(-q, y, x), r, q);
+}
+
+// fdiv with IEEE's result for a zero or infinite operand (round 6): where the
+// divisor can be zero in the physics -- kappa / log((z - h_snow)/z0) of :670 at
+// h_snow = z - z0, where the reference's quotient is inf -- fdiv's NaN is
+// replaced by the IEEE quotient behind one rare test (NaN operands stay NaN).
+TFG_FM_HD inline double fdiv_z(double x, double y) {
+  double q = fdiv(x, y);
+  if (__builtin_expect(q != q, 0)) {
+    TFG_FM_RARE();
+    q = x / y;
+  }
+  return q;
 }
 
 // ---------------------------------------------------------------------------

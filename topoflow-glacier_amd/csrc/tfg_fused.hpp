@@ -156,12 +156,20 @@ __device__ __forceinline__ void wave_flush(double* __restrict__ wbins, int cid, 
                       // (100 MHz) at start and end and the XCC / CU it ran on
 static __device__ unsigned long long g_wg_times[TFG_WG_TIMING][3];
 #endif
-constexpr int kMinWaves = 4;       // __launch_bounds__ minimum waves per SIMD: fp32 engine, <= 128 VGPRs
+#ifndef TFG_MIN_WAVES
+#define TFG_MIN_WAVES 4
+#endif
+constexpr int kMinWaves = TFG_MIN_WAVES;  // __launch_bounds__ minimum waves per SIMD: fp32 engine, <= 128 VGPRs
 constexpr int kMinWavesExact = 2;  // fp64 engine: 256 VGPRs, no scratch spills
+#ifndef TFG_MIN_WAVES_PREC
+#define TFG_MIN_WAVES_PREC 4
+#endif
+constexpr int kMinWavesPrec = TFG_MIN_WAVES_PREC;  // fp32 engine's fp64-flux form
 // NS (fast engine only): the NaN-safe form of the step (tfg::cell_step_fast),
-// for launches the host could not verify to read only finite values.
-template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false>
-__global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : kMinWaves) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
+// for launches the host could not verify to read only finite values.  PREC
+// (fast engine only): the fp64 flux form (tfg_set_flux(TFG_FLUX_F64)).
+template <class R, bool EXACT, bool READ_DEPTHS, bool CATCH, bool QC, int C, bool NS = false, bool PREC = false>
+__global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesPrec : kMinWaves)) void k_fused(const KArgs a, const tfg_uniforms* __restrict__ uni,
                                                   const R* __restrict__ forc,      // [n_frames][5][n_pad]
                                                   const R* __restrict__ stat,      // [3][n_pad]
                                                   const float* __restrict__ geo,   // [kGeoF][n_pad] f32 + [2][n_pad] f64
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : kMinWaves) void k_
             o_im[j] = (R)o.IM; o_mt[j] = (R)o.M_total; o_rh[j] = (R)o.RH;
           } else {
             tfg::CellOutF o;
-            tfg::cell_step_fast<QC, NS>(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j],
+            tfg::cell_step_fast<QC, NS, PREC>(p, SF[j], up, u, geo_d, n_pad, c0 + j, (float)f.P[j], (float)f.T[j],
                                         (float)f.Q[j], (float)f.PA[j], (float)f.UZ[j], f.q[j], qn[j], cs[j], o, df[j],
                                         (float)qc[j]);
             o_hs[j] = (R)o.h_snow; o_sm[j] = (R)o.SM; o_hi[j] = (R)o.h_ice;
@@ -355,7 +363,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : kMinWaves) void k_
       // so a fused launch needs ring_len > 2 (launch_steps runs shorter windows
       // one step per launch).  The conduction (QC) and NaN-safe (NS) forms keep
       // one step ahead: with two they spill 2-4 VGPRs.
-      constexpr int kAhead = (QC || NS) ? 1 : kPrefetchFast;
+      constexpr int kAhead = (QC || NS || PREC) ? 1 : kPrefetchFast;
       Frame fa, fb;
       fetch(0, fa);
       if constexpr (EXACT) {
@@ -510,5 +518,9 @@ struct FusedBufs {
 // (read_depths, catchments, qc_on) on `stream`.
 hipError_t launch_fused_exact(const KArgs& a, const FusedBufs& b, bool read_depths, bool catchments, bool qc_on,
                               int blocks, size_t lds, hipStream_t stream);
+// The fp32 engine's fp64-flux form (tfg_fused_prec.hip): the instantiation for
+// (read_depths, catchments, qc_on, nan_safe) on `stream`.
+hipError_t launch_fused_prec(const KArgs& a, const FusedBufs& b, bool read_depths, bool catchments, bool qc_on,
+                             bool nan_safe, int blocks, size_t lds, hipStream_t stream);
 
 }  // namespace tfg_kern

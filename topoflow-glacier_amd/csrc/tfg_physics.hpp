@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "tfg_fastmath.hpp"
 
 namespace tfg {
@@ -89,6 +91,12 @@ struct DevParams {
   float f_em_sc;              // 0.1 * 2^10: em_air's (e/T)^(1/7) = (e f_em_sc / T)^(1/7) 2^(-10/7)  :1167
   float f_ccFs;               // (1-F)*1.72*(1+0.22C^2) * 2^(-10/7)            :1167-1175
   float f_Fm1;                // F - 1: em_air - 1 for the long-wave balance
+  // fast variant's fp64 turbulent chain (round 6)
+  double d_eps100, d_ome100;  // 100 eps, 100 (1 - eps): e_air [mbar] = Q P_air / (d_eps100 + d_ome100 Q)   :817-826
+  double d_k2;                // (kappa / ln 2)^2: Dn = uz d_k2 / log2((z - h)/z0)^2                       :670-672
+  double d_l2k, d_l2kk;       // k, k^2 of the scaled roughness log (f_inv_z0s)
+  double d_qe;                // rho_air Lv lhc 100 / sea_p0                                               :931-934
+  double d_es_k, d_es_c;      // e_sat(T_s) / e_sat(T_a) = exp(-d_es_k dTs / ((T_s + c)(T_a + c))), c = d_es_c  :788-807
 };
 
 // Per-cell static quantities derived from elev/slope/aspect (set_aspect_angle
@@ -540,7 +548,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
   // :670-726
-  const double arg = fdiv(p.kappa, log_k(npmax(div_r(p.z - h_snow, p.inv_z0), 0.01)));
+  const double arg = tfg_fm::fdiv_z(p.kappa, log_k(npmax(div_r(p.z - h_snow, p.inv_z0), 0.01)));
   const double Dn = uz * (arg * arg);
   const double Dh = stability_dh(Dn, top, bot);
   // :744-745
@@ -723,7 +731,7 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
   const double top = p.gz * (T_air - T_surf);
   double bot = (uz * uz) * (T_air + 273.15);
   if (bot == 0.0) bot = 0.01;
-  const double arg = fdiv(p.kappa, log_dn);
+  const double arg = tfg_fm::fdiv_z(p.kappa, log_dn);  // inf at h_snow = z - z0, as the reference
   const double Dn = uz * (arg * arg);
   const double Dh = stability_dh(Dn, top, bot);
   const double Qh = p.rho_air_Cp_air * Dh * (T_air - T_surf);
@@ -747,8 +755,8 @@ __device__ inline void cell_step_exact_wave(const DevParams& p, const CellStatic
     ex2 = exp_k(ea2);
   }
   if (X.mine(X_POW2) && p.satterlund) pw2 = pow(opaque(10.0), 11.4 - fdiv(2353.0, T_surf + 273.15));  // :796 (surface)
-  // Stull wet bulb (:1514-1520), only where it snows: wet_bulb_parts' two arguments and, for RH > 8,
-  // the small term's own arctangent
+  // Stull wet bulb (:1514-1520), only where it snows: wet_bulb_parts' two arguments and, for RH
+  // outside [0, 5] (stull_off_fit), the arctangents off the fits
   double wb_u0 = 0.0, wb_num = 0.0, wb_den = 1.0;
   if (P_snow > 0.0) wet_bulb_parts(T_air, RH, wb_u0, wb_num, wb_den);
   if (X.mine(X_ATAN2) && P_snow > 0.0) at2 = atan(lane == 2 ? 0.023101 * RH : wb_u0);
@@ -994,13 +1002,14 @@ struct MeltF {
   double h_swe, h_iwe, Eccs, Ecci;
   float SM, IM, Erem_s, IM_int;  // outputs; terms of the SM and IM integrals (:1486, :1493)
 };
-template <bool NS>
-__device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, float P_snow, float RH, float T_air,
+template <bool NS, class QT>
+__device__ __forceinline__ MeltF melt_core(const DevParams& p, QT Q_sum, float P_snow, float RH, float T_air,
                                            double h_swe0, double h_iwe0, double Eccs0, double Ecci0,
                                            double h_ice_prev) {
   MeltF m;
   const double previous_swe = h_swe0;
-  const double E_in = (double)(Q_sum * p.f_dt);  // dt in hours, as the reference (:1364)
+  // dt in hours, as the reference (:1364); an fp64 Q_sum (the PREC form) times the fp64 dt
+  const double E_in = sizeof(QT) == 8 ? (double)Q_sum * p.dt : (double)(Q_sum * p.f_dt);
   // snow melt (:1364-1373; max(SM, 0) is implied by E_rem >= 0), integral (:1486)
   const double E_rem_s = dmax<NS>(E_in - Eccs0, 0.0);
   m.Erem_s = (float)E_rem_s;
@@ -1035,10 +1044,10 @@ __device__ __forceinline__ MeltF melt_core(const DevParams& p, float Q_sum, floa
   m.IM = (float)IM;
   return m;
 }
-template <bool NS>
-__device__ __forceinline__ void melt_fast(const DevParams& p, float Q_sum, float P_snow, float P_rain, float RH,
+template <bool NS, class QT>
+__device__ __forceinline__ void melt_fast(const DevParams& p, QT Q_sum, float P_snow, float P_rain, float RH,
                                           float T_air, CellState& st, CellOutF& o, DiagF& d) {
-  const MeltF m = melt_core<NS>(p, Q_sum, P_snow, RH, T_air, st.h_swe, st.h_iwe, st.Eccs, st.Ecci, st.h_ice);
+  const MeltF m = melt_core<NS, QT>(p, Q_sum, P_snow, RH, T_air, st.h_swe, st.h_iwe, st.Eccs, st.Ecci, st.h_ice);
   d.Erem_s += m.Erem_s;
   d.IM += m.IM_int;
   // depths (:1711, :1726)
@@ -1058,7 +1067,11 @@ __device__ __forceinline__ void melt_fast(const DevParams& p, float Q_sum, float
   o.RH = RH;
 }
 
-template <bool QC, bool NANSAFE>
+// PREC (round 6): the dew point, the turbulent fluxes and the long-wave balance
+// in fp64 (tfg_set_flux(TFG_FLUX_F64)).  Eccs integrates E_in over a cold spell
+// and SM reads E_in - Eccs at melt onset, where the fp32 rounding of those
+// terms adds up; the fp32 form is the default.
+template <bool QC, bool NANSAFE, bool PREC = false>
 __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, const tfg_uniforms* __restrict__ up,
                                       const tfg_uniforms& u, const double* __restrict__ geo_d, int64_t n_pad,
                                       int64_t cell, float P, float T_air, float Hum_sp, float P_air, float uz,
@@ -1086,37 +1099,71 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   } else {
     inv_esat = 100.0f * fexp2((2353.0f * rT - 11.4f) * 3.3219280948873626f);
   }
-  const float e_air = Hum_sp * P_air * frcp_nr(p.f_eps100 + p.f_ome100 * Hum_sp);
-  // dew point (:888-893) and surface temperature (:906-910).  ln(e_air /
-  // 6.1121) as the log of the ratio (~1) and Newton-refined: no bias of
-  // v_log_f32 reaches T_dew, which every flux term reads
-  const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
-  const float T_dew = 257.14f * log_term * frcp_nr(18.678f - log_term);
-  const float T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
+  // dew point (:888-893), surface temperature (:906-910), T_air - T_surf
+  double Td = T_air, e64 = 0.0, Tsd = 0.0, dTd = 0.0;
+  float e_air, T_dew, T_surf, dTs;
+  if constexpr (PREC) {
+    e64 = ((double)Hum_sp * (double)P_air) * rcp_nr1(fma((double)Hum_sp, p.d_ome100, p.d_eps100));
+    const double Ld = tfg_fm::log_k(e64 * (1.0 / 6.1121));
+    const double Tdew = (257.14 * Ld) * rcp_nr1(18.678 - Ld);
+    Tsd = (snow_pos || ice_pos) ? dmin<NS>(Tdew, 0.0) : Tdew;
+    dTd = Td - Tsd;
+    e_air = (float)e64;
+    T_dew = (float)Tdew;
+    T_surf = (float)Tsd;
+    dTs = (float)dTd;
+  } else {
+    e_air = Hum_sp * P_air * frcp_nr(p.f_eps100 + p.f_ome100 * Hum_sp);
+    // ln(e_air / 6.1121) as the log of the ratio (~1) and Newton-refined: no
+    // bias of v_log_f32 reaches T_dew, which every flux term reads
+    const float log_term = flog2_nr(e_air * (1.0f / 6.1121f)) * kLn2;
+    T_dew = 257.14f * log_term * frcp_nr(18.678f - log_term);
+    T_surf = (snow_pos || ice_pos) ? nmin<NS>(T_dew, 0.0f) : T_dew;
+    dTs = T_air - T_surf;
+  }
   const float RH = e_air * inv_esat;
   // turbulent fluxes (:640-745, :919-934)
-  const float dTs = T_air - T_surf;
-  float bot = (uz * uz) * T_K;
-  if (bot == 0.0f) bot = 0.01f;
-  const float Ri = p.f_gz * dTs * frcp(bot);
   // log2((z - h_snow)/z0) = ly + k with ly = log2((z - h_snow) 2^-k / z0) ~ 0
   // (k = round(log2(z/z0)), host side): squared as ly (ly + 2k) + k^2, so
   // v_log_f32's error is relative to ly, not to the whole log (~13)
   const float ly2 = flog2(nmax<NS>((p.f_z - (float)st.h_snow) * p.f_inv_z0s, p.f_l2min));
-  const float L2sq = fmaf(ly2, ly2 + p.f_l2k2, p.f_l2kk);
-  const float Dn = uz * p.f_k2 * frcp(L2sq);
-  const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
-  // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
-  // (:853), written without the cancellation of the two near-equal pressures:
-  //   e_air - e_surf = e_air*(1 - 2^x2),  x2 = -k*log2(e)*dTs/((T_s+c)(T_a+c))
-  // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15):
-  // one unbiased exp2 of the exponent difference, so the remaining error is
-  // random (v_exp_f32 rounding), not a bias that would accumulate in Eccs
-  const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
-  const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;
-  const float de = fmaf(-e_air, fexp2(xs2), e_air);
-  const float Qh = p.f_rho_air_Cp_air * Dh * dTs;
-  const float Qe = p.f_qe * Dh * de * fexp2(g.ek * rT);  // lhc / p0 folded
+  std::conditional_t<PREC, double, float> Qh, Qe;
+  if constexpr (PREC) {
+    const double uzd = uz;
+    double botd = (uzd * uzd) * (Td + 273.15);
+    if (botd == 0.0) botd = 0.01;
+    const double top = p.gz * dTd;
+    const double L2 = fma((double)ly2, (double)ly2 + 2.0 * p.d_l2k, p.d_l2kk);
+    // Dh = Dn / (1 + 10 Ri) or Dn (1 - 10 Ri), Ri = top / bot: one quotient (stability_dh)
+    const bool stable = top > 0.0;
+    const double num = stable ? botd : fma(-10.0, top, botd);
+    const double den = stable ? fma(10.0, top, botd) : botd;
+    const double Dhd = (uzd * p.d_k2) * num * rcp_nr1(L2 * den);
+    Qh = (p.rho_air_Cp_air * Dhd) * dTd;
+    // e_air - e_surf = e_air (1 - e_sat(T_s) / e_sat(T_a)), the exponent difference in one exp
+    const double x_es = (-p.d_es_k * dTd) * rcp_nr1((Tsd + p.d_es_c) * (Td + p.d_es_c));
+    const double ded = e64 * (1.0 - tfg_fm::exp_k(x_es));
+    const double p0f = tfg_fm::exp_k(((double)g.ek * 0.69314718055994531) * rcp_nr1(Td + 273.15));  // lhc / p0
+    Qe = (p.d_qe * Dhd) * ded * p0f;
+  } else {
+    float bot = (uz * uz) * T_K;
+    if (bot == 0.0f) bot = 0.01f;
+    const float Ri = p.f_gz * dTs * frcp(bot);
+    const float L2sq = fmaf(ly2, ly2 + p.f_l2k2, p.f_l2kk);
+    const float Dn = uz * p.f_k2 * frcp(L2sq);
+    const float Dh = (Ri > 0.0f) ? Dn * frcp(fmaf(10.0f, Ri, 1.0f)) : Dn * fmaf(-10.0f, Ri, 1.0f);
+    // e_air - e_surf with e_surf = RH*e_sat_surf = e_air*e_sat(T_surf)/e_sat(T_air)
+    // (:853), written without the cancellation of the two near-equal pressures:
+    //   e_air - e_surf = e_air*(1 - 2^x2),  x2 = -k*log2(e)*dTs/((T_s+c)(T_a+c))
+    // (Brutsaert k = 17.3*237.3, c = 237.3; Satterlund k = 2353 ln 10, c = 273.15):
+    // one unbiased exp2 of the exponent difference, so the remaining error is
+    // random (v_exp_f32 rounding), not a bias that would accumulate in Eccs
+    const float rS = frcp(T_surf + (p.satterlund ? 273.15f : 237.3f));
+    const float xs2 = (p.satterlund ? -7816.4968f : -5922.6815f) * dTs * rS * rA;
+    const float de = fmaf(-e_air, fexp2(xs2), e_air);
+    Qh = p.f_rho_air_Cp_air * Dh * dTs;
+    Qe = p.f_qe * Dh * de * fexp2(g.ek * rT);  // lhc / p0 folded
+  }
   // snowfall window + albedo ageing (:1006-1059)
   {
     const float sq = P_snow * p.f_qfac;  // P_snow*dt*ws*2^36
@@ -1181,32 +1228,52 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   // longwave (:1167-1248): em_air - 1 (the balance below needs only that)
   float em_m1;
   if (!p.satterlund) {
-    // (e_air / (10 T_K))^(1/7) as (e_air 102.4 / T_K)^(1/7) 2^(-10/7): the
-    // scaled argument is ~1, so v_log_f32's relative error stays off the root
-    const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));
-    em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);  // (1-F) 1.72 (1+0.22C^2) root + F - 1
+    if constexpr (PREC) {
+      em_m1 = 0.0f;  // fp64 below
+    } else {
+      // (e_air / (10 T_K))^(1/7) as (e_air 102.4 / T_K)^(1/7) 2^(-10/7): the
+      // scaled argument is ~1, so v_log_f32's relative error stays off the root
+      const float em_r = fexp2(flog2(e_air * p.f_em_sc * rT) * (1.0f / 7.0f));
+      em_m1 = fmaf(p.f_ccFs, em_r, p.f_Fm1);  // (1-F) 1.72 (1+0.22C^2) root + F - 1
+    }
   } else {
     em_m1 = 1.08f * (1.0f - fexp2(-kLog2e * fexp2(flog2(e_air) * (T_K * (1.0f / 2016.0f))))) - 1.0f;
   }
   // em Ta^4 - Ts^4 without its cancellation (LW_in ~ LW_out ~ 300 W m-2, net
   // ~100): (em - 1) Ta^4 + (Ta - Ts)(Ta + Ts)(Ta^2 + Ts^2), with Ta - Ts the
   // degC difference dTs (free of the rounding of the two +273.15 sums)
-  const float T_surf_K = T_surf + 273.15f;
-  const float ta2 = T_K * T_K;
-  const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
-  const float Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
-  float Q_sum = Qn_SW + Qn_LW + Qh + Qe;
-  if constexpr (QC) Q_sum = Q_sum + qc;  // :1314, Qc last (Qa = 0)
+  std::conditional_t<PREC, double, float> Qn_LW;
+  if constexpr (PREC) {
+    // em_air's seventh root by one Halley step from an fp32 seed (root7, the
+    // fp64 engine's; Satterlund's em_air stays fp32), the balance in fp64
+    const double TaK = Td + 273.15, TsK = Tsd + 273.15;
+    const double emd_m1 = p.satterlund ? (double)em_m1
+                                       : fma(p.one_minus_F_172 * p.cloud_term, root7((e64 * 0.1) * rcp_nr1(TaK)), p.F - 1.0);
+    const double ta2d = TaK * TaK;
+    Qn_LW = p.em_surf_sigma * fma(emd_m1, ta2d * ta2d, dTd * (TaK + TsK) * fma(TsK, TsK, ta2d));
+  } else {
+    const float T_surf_K = T_surf + 273.15f;
+    const float ta2 = T_K * T_K;
+    const float d4 = dTs * (T_K + T_surf_K) * fmaf(T_surf_K, T_surf_K, ta2);
+    Qn_LW = p.f_em_surf_sigma * fmaf(em_m1, ta2 * ta2, d4);
+  }
+  // :1314 (Qa = 0; Qc last): fp64 in the PREC form, E_in = Q_sum dt then in fp64
+  std::conditional_t<PREC, double, float> Q_sum;
+  if constexpr (PREC) Q_sum = (((double)Qn_SW + Qn_LW) + Qh) + Qe + (QC ? (double)qc : 0.0);
+  else {
+    Q_sum = Qn_SW + Qn_LW + Qh + Qe;
+    if constexpr (QC) Q_sum = Q_sum + qc;
+  }
 
-  melt_fast<NS>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
+  melt_fast<NS, decltype(Q_sum)>(p, Q_sum, P_snow, P_rain, RH, T_air, st, o, d);
 #if defined(TFG_DEBUG_TERMS)  // diagnostic builds only (tests/diagnostics/term_bias.py): the step's
                               // energy terms replace the six outputs; the state evolves as usual
   o.h_snow = Qn_SW;
-  o.SM = Qn_LW;
-  o.h_ice = Qh;
-  o.IM = Qe;
+  o.SM = (float)Qn_LW;
+  o.h_ice = (float)Qh;
+  o.IM = (float)Qe;
   o.M_total = P_snow > 0.0f ? snowfall_cold(p, P_snow, RH, T_air) : 0.0f;
-  o.RH = Q_sum;
+  o.RH = (float)Q_sum;
 #endif
 }
 

@@ -20,7 +20,7 @@ __all__ = [
 
 LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
 
-ABI_VERSION = 6  # include/tfg.h TFG_ABI_VERSION
+ABI_VERSION = 7  # include/tfg.h TFG_ABI_VERSION
 FLOW_ALL, FLOW_INTERIOR, FLOW_EDGES = 0, 1, 2  # tfg_ice_flow_step parts
 PREV_DEPTH = -1  # tfg_get_field / tfg_set_field index: the fp64 previous-step depth (TFG_PREV_DEPTH)
 F32, F64, I32 = 0, 1, 2
@@ -125,6 +125,7 @@ def load() -> ctypes.CDLL:
         "tfg_conduction_off": ([vp], i32),
         "tfg_nan_safe_launches": ([vp, ctypes.POINTER(i64)], i32),
         "tfg_set_step_form": ([vp, i32], i32),
+        "tfg_set_flux": ([vp, i32], i32),
         "tfg_selftest_powers": ([i32, vp, i64, i32, vp], i32),
     }
     for name, (args, res) in sigs.items():
@@ -167,8 +168,9 @@ def code_object_sha256(path: Path | None = None) -> str | None:
     return hashlib.sha256(blob).hexdigest() if blob else None
 
 
-BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0E"  # k_fused<float, false, false, false, false, 1, false>
-BENCH_KERNEL_F64 = "_ZN8tfg_kern7k_fusedIdLb1ELb0ELb0ELb0ELi1ELb0E"  # k_fused<double, true, false, false, false, 1, false>
+BENCH_KERNEL = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0ELb0E"  # k_fused<float, false, false, false, false, 1, false, false>
+BENCH_KERNEL_PREC = "_ZN8tfg_kern7k_fusedIfLb0ELb0ELb0ELb0ELi1ELb0ELb1E"  # ... the fp64-flux form (PREC = true)
+BENCH_KERNEL_F64 = "_ZN8tfg_kern7k_fusedIdLb1ELb0ELb0ELb0ELi1ELb0ELb0E"  # k_fused<double, true, false, false, false, 1, false, false>
 
 
 def gfx950_code_objects(path: Path | None = None) -> list[bytes]:
@@ -290,5 +292,5 @@ def exported_symbols() -> list[str]:
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update", "tfg_update_many", "tfg_conduction_edges", "tfg_conduction_update", "tfg_conduction_off",
-        "tfg_nan_safe_launches", "tfg_set_step_form", "tfg_selftest_powers",
+        "tfg_nan_safe_launches", "tfg_set_step_form", "tfg_set_flux", "tfg_selftest_powers",
     ) if hasattr(L, n)]

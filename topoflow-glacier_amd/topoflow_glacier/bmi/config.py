@@ -16,6 +16,10 @@ deliberate, additive differences:
   float32 for grids), ``device`` (HIP device ordinal, default LOCAL_RANK or 0),
   ``time_zone`` (IANA name; default looked up from lat/lon),
   ``fuse_steps`` (time steps fused per kernel launch, default 24),
+  ``flux_precision`` ("fp32" | "fp64": the float32 engine's energy-flux
+  arithmetic; "fp64" computes the dew point, turbulent fluxes and long-wave
+  balance in fp64 so the cold content carries no fp32 rounding into melt
+  onset, at a measured throughput cost; default "fp32"),
   ``ice_flow`` / ``ice_flow_interval`` / ``dx`` / ``dy`` (the optional
   shallow-ice flow term, off by default; it moves ice between cells every
   ``ice_flow_interval`` steps on a grid of dx x dy metre cells) and
@@ -119,6 +123,7 @@ class TopoflowGlacierConfig(BaseModel):
     device: int | None = None
     time_zone: str | None = None
     fuse_steps: int = Field(24, ge=1)
+    flux_precision: Literal["fp32", "fp64"] = "fp32"  # the float32 engine's flux arithmetic (tfg_set_flux)
     # optional lateral ice flow (extension; tfg_ice_flow_*): off by default,
     # which keeps results identical to the reference
     ice_flow: bool = False

@@ -46,7 +46,7 @@ class GlacierEngine:
 
     def __init__(self, cfg, ny: int, nx: int, engine: str = "float32", device: int | None = None,
                  n_frames: int = 1, hist_depth: int = 1, n_catch: int = 1, fuse_steps: int | None = None,
-                 row0: int = 0):
+                 row0: int = 0, flux: str | None = None):
         self.lib = nat.load()
         self.cfg = cfg
         self.ny, self.nx, self.n = int(ny), int(nx), int(ny) * int(nx)
@@ -66,6 +66,11 @@ class GlacierEngine:
         self.h = h
         self.fuse_steps = int(fuse_steps or getattr(cfg, "fuse_steps", 24) or 24)
         nat.check(self.lib.tfg_set_fuse(self.h, self.fuse_steps), self.h)
+        # the float32 engine's flux arithmetic (tfg_set_flux): the argument, else the config's flux_precision
+        self.flux = flux or getattr(cfg, "flux_precision", None) or "fp32"
+        if self.flux not in ("fp32", "fp64"):
+            raise ValueError(f"flux must be 'fp32' or 'fp64', not {self.flux!r}")
+        nat.check(self.lib.tfg_set_flux(self.h, 1 if self.flux == "fp64" else 0), self.h)
         self.clock = StepClock(cfg.start_time, cfg.dt, cfg.lat, cfg.lon, getattr(cfg, "time_zone", None),
                                ring_len=self.ring_len)
         self.step_index = 0  # model steps completed
