@@ -669,6 +669,11 @@ struct tfg_handle {
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
   bool force_ns = false;             // tfg_set_step_form(TFG_FORM_NAN_SAFE): every launch NaN-safe
   bool flux_f64 = false;             // tfg_set_flux(TFG_FLUX_F64): the fp32 engine's fp64-flux form
+  // a small grid's launches run as two halves on two streams (launch_steps):
+  // the second stream and the fork / join events, made on first use
+  hipStream_t side_stream = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  int resident_blocks = 0;           // k_fused workgroups resident on the device at once
   std::string err;
 };
 
@@ -931,9 +936,16 @@ struct IoArgs {
   uint8_t in_state = kUnknown;  // the inputs' finite-data status (tfg_handle::plane_state)
 };
 
+// One k_fused launch on `stream` over the cell groups [g_lo, g_hi) (g_hi = 0:
+// the whole plane stride), its workgroups accumulating into the slab rows from
+// slab_row0 on.
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns) {
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns,
+                 hipStream_t stream, int64_t g_lo = 0, int64_t g_hi = 0, int slab_row0 = 0) {
   KArgs a;
+  a.g_lo = g_lo;
+  a.g_hi = g_hi;
+  a.slab_row0 = slab_row0;
   a.p = h->dp;
   a.K = K;
   a.io_in = io.in;
@@ -948,20 +960,20 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   if constexpr (EXACT) {  // the fp64 engine's instantiations live in tfg_fused_f64.hip
     const FusedBufs fb = {d_u, h->forc, h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->slab,
                           h->qc};
-    HIPCHK(h, launch_fused_exact(a, fb, rd, ct, h->qc_on, blocks, lds, h->stream));
+    HIPCHK(h, launch_fused_exact(a, fb, rd, ct, h->qc_on, blocks, lds, stream));
     return TFG_OK;
   } else {
   if (h->flux_f64) {  // the fp64-flux form's instantiations live in tfg_fused_prec.hip
     const FusedBufs fb = {d_u, h->forc, h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->slab,
                           h->qc};
-    HIPCHK(h, launch_fused_prec(a, fb, rd, ct, h->qc_on, ns, blocks, lds, h->stream));
+    HIPCHK(h, launch_fused_prec(a, fb, rd, ct, h->qc_on, ns, blocks, lds, stream));
     return TFG_OK;
   }
   constexpr int C = kCellsPerThread;
 #define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, \
                  h->slab, (const R*)h->qc
 #define TFG_LAUNCH(RD, CT, QC, NS) \
-  hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C, NS>), blocks, kBlock, lds, h->stream, TFG_ARGS)
+  hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C, NS>), blocks, kBlock, lds, stream, TFG_ARGS)
 #define TFG_LAUNCH_NS(RD, CT, QC) \
   do { if (ns) TFG_LAUNCH(RD, CT, QC, true); else TFG_LAUNCH(RD, CT, QC, false); } while (0)
   if (h->qc_on) {  // the optional lateral conduction term (tfg_conduction_update / TFG_ST_QC)
@@ -1088,6 +1100,8 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // section 5).  The per-workgroup diagnostic slab is kept under 256 MiB for
   // large catchment counts: 65536 workgroups at config 5's 43 catchments
   // (135 MB), +1.2 % on its slab against the 16384 a 64 MiB cap gave.
+  // k_fused runs 4 waves per SIMD (__launch_bounds__): 4 workgroups of kWaves waves per CU
+  h->resident_blocks = prop.multiProcessorCount * (4 * 4 / kWaves);
   h->max_blocks = std::max(256, prop.multiProcessorCount * 512);
   h->max_blocks = (int)std::max<int64_t>(256, std::min<int64_t>(h->max_blocks, (256ll << 20) / ((int64_t)n_catch * 6 * 8)));
   // a power of two: with many catchments a slab-capped odd count (31775 at 44
@@ -1147,6 +1161,12 @@ int tfg_destroy(tfg_handle* h) {
   if (h->out_d) (void)hipFree(h->out_d);
   if (h->out_h) (void)hipHostFree(h->out_h);
   if (h->io_h) (void)hipHostFree(h->io_h);
+  if (h->side_stream) {
+    (void)hipStreamSynchronize(h->side_stream);
+    (void)hipStreamDestroy(h->side_stream);
+  }
+  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return TFG_OK;
@@ -1522,6 +1542,29 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
   return TFG_OK;
 }
 
+// A launch of the fp32 engine as two halves of the cell groups, the first on
+// the handle's stream and the second on a side stream forked from and joined
+// back into it (stream order for the caller is unchanged); each half's
+// workgroups accumulate into their own slab rows, so the diagnostics stay
+// deterministic.
+int launch_split(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, bool ns) {
+  if (!h->side_stream) {
+    HIPCHK(h, hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+  }
+  const int64_t chunks = (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock;
+  const int64_t mid = (chunks / 2) * kBlock;  // cell groups, a whole number of chunks
+  const int b0 = blocks / 2, b1 = blocks - blocks / 2;
+  HIPCHK(h, hipEventRecord(h->fork_ev, h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->side_stream, h->fork_ev, 0));
+  if (int rc = launch_fused<float, false>(h, d_u, K, b0, lds, IoArgs(), ns, h->stream, 0, mid, 0)) return rc;
+  if (int rc = launch_fused<float, false>(h, d_u, K, b1, lds, IoArgs(), ns, h->side_stream, mid, 0, b0)) return rc;
+  HIPCHK(h, hipEventRecord(h->join_ev, h->side_stream));
+  HIPCHK(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
+  return TFG_OK;
+}
+
 int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
                  const IoArgs& io = IoArgs()) {
   if (int rc = prepare_steps(h)) return rc;
@@ -1532,6 +1575,15 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   // (see the prefetch note in k_fused)
   const int fuse = h->ring_len > (h->engine == TFG_F32 ? kPrefetchFast : 1) ? h->fuse : 1;
   const bool one_cell = h->engine == TFG_F64 && h->n == 1 && !io.in;  // k_cell_run
+  // a grid of 2 to 4 rounds of resident workgroups (1024^2 cells on the
+  // MI355X: 4096 workgroups, 4 rounds of 1024) idles ~10 % of each launch in
+  // its drain; two half launches on two streams fill each other's drain
+  // (HISTORY.md section 10; fp32 engine, launches without tfg_update's host I/O)
+#ifndef TFG_SPLIT_SMALL  // measurement builds: -DTFG_SPLIT_SMALL=0 runs every grid as one launch
+#define TFG_SPLIT_SMALL 1
+#endif
+  const bool split = TFG_SPLIT_SMALL && h->engine == TFG_F32 && !io.in && blocks >= 2 * h->resident_blocks &&
+                     blocks <= 4 * h->resident_blocks;
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
     int rc = TFG_OK;
@@ -1554,14 +1606,14 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
     } else if (h->engine == TFG_F32) {
       bool ns = true;
       if ((rc = choose_form(h, u + k0, K, io, &ns))) return rc;
-      rc = launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, ns);
+      rc = split ? launch_split(h, d_u + k0, K, blocks, lds, ns) : launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, ns, h->stream);
       if (ns) {
         ++h->ns_launches;
         // the NaN-safe form may have carried missing data into the state
         if (h->state_state == kOk) h->state_state = kUnknown;
       }
     } else {
-      rc = launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, false);
+      rc = launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, false, h->stream);
     }
     if (rc) return rc;
     h->depths_derived = true;
