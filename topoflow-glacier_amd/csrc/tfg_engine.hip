@@ -936,15 +936,15 @@ struct IoArgs {
   uint8_t in_state = kUnknown;  // the inputs' finite-data status (tfg_handle::plane_state)
 };
 
-// One k_fused launch on `stream` over the cell groups [g_lo, g_hi) (g_hi = 0:
-// the whole plane stride), its workgroups accumulating into the slab rows from
-// slab_row0 on.
+// One k_fused launch on `stream` over the chunks [chunk0, chunk0 + nchunks) of
+// kBlock cell groups (nchunks = 0: the whole plane stride), its workgroups
+// accumulating into the slab rows from slab_row0 on.
 template <class R, bool EXACT>
 int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns,
-                 hipStream_t stream, int64_t g_lo = 0, int64_t g_hi = 0, int slab_row0 = 0) {
+                 hipStream_t stream, int chunk0 = 0, int nchunks = 0, int slab_row0 = 0) {
   KArgs a;
-  a.g_lo = g_lo;
-  a.g_hi = g_hi;
+  a.chunk0 = chunk0;
+  a.nchunks = nchunks;
   a.slab_row0 = slab_row0;
   a.p = h->dp;
   a.K = K;
@@ -1553,13 +1553,13 @@ int launch_split(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
     HIPCHK(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
     HIPCHK(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
   }
-  const int64_t chunks = (h->n_pad / kCellsPerThread + kBlock - 1) / kBlock;
-  const int64_t mid = (chunks / 2) * kBlock;  // cell groups, a whole number of chunks
+  const int chunks = (int)((h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);  // <= 4 rounds of workgroups
+  const int c0 = chunks / 2;
   const int b0 = blocks / 2, b1 = blocks - blocks / 2;
   HIPCHK(h, hipEventRecord(h->fork_ev, h->stream));
   HIPCHK(h, hipStreamWaitEvent(h->side_stream, h->fork_ev, 0));
-  if (int rc = launch_fused<float, false>(h, d_u, K, b0, lds, IoArgs(), ns, h->stream, 0, mid, 0)) return rc;
-  if (int rc = launch_fused<float, false>(h, d_u, K, b1, lds, IoArgs(), ns, h->side_stream, mid, 0, b0)) return rc;
+  if (int rc = launch_fused<float, false>(h, d_u, K, b0, lds, IoArgs(), ns, h->stream, 0, c0, 0)) return rc;
+  if (int rc = launch_fused<float, false>(h, d_u, K, b1, lds, IoArgs(), ns, h->side_stream, c0, chunks - c0, b0)) return rc;
   HIPCHK(h, hipEventRecord(h->join_ev, h->side_stream));
   HIPCHK(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
   return TFG_OK;

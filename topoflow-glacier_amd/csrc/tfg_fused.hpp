@@ -52,10 +52,10 @@ struct KArgs {
   double* io_out;
   uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
   uint32_t io_seq;
-  // the cell groups [g_lo, g_hi) this launch steps (a multiple of kBlock
-  // apart; g_hi = 0: the whole plane stride) and its first slab row: a small
-  // grid runs as two such launches on two streams (launch_steps)
-  int64_t g_lo = 0, g_hi = 0;
+  // the chunks of kBlock cell groups this launch steps, [chunk0, chunk0 +
+  // nchunks) (nchunks = 0: the whole plane stride), and its first slab row: a
+  // small grid runs as two such launches on two streams (launch_split)
+  int chunk0 = 0, nchunks = 0;
   int slab_row0 = 0;
 };
 
@@ -198,15 +198,14 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
   const int64_t n_pad = a.n_pad;
   // the whole plane stride, the skew's padding cells included (stepping only the cells
   // measured neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, profiles/r4d_ab_skew.json)
-  const int64_t glo = a.g_lo, ghi = a.g_hi > 0 ? a.g_hi : n_pad / C;
-  const int64_t ngroups = ghi - glo;
+  const int64_t ngroups = n_pad / C;
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
-  const int64_t nchunks = (ngroups + kBlock - 1) / kBlock;
+  const int64_t nchunks = a.nchunks > 0 ? a.nchunks : (ngroups + kBlock - 1) / kBlock;
   const int64_t wg = blockIdx.x;
-  const int64_t g0 = glo + (wg * nchunks / gridDim.x) * kBlock;
-  const int64_t g1 = std::min<int64_t>(glo + ((wg + 1) * nchunks / gridDim.x) * kBlock, ghi);
+  const int64_t g0 = (a.chunk0 + wg * nchunks / gridDim.x) * kBlock;
+  const int64_t g1 = std::min<int64_t>((a.chunk0 + (wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
   const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad);
 
