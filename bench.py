@@ -65,18 +65,21 @@ def bytes_model(elem: int = 4, catchments: bool = False, qc: bool = False) -> tu
       per step:   forcing 5 x elem read, window slot 4 read + 4 written, six
                   outputs 6 x elem written  (fp32 52 B, fp64 96 B);
       per launch: geometry (fp32 engine five f32 planes, fp64 engine seven f64
-                  planes), state six f64 + window total i64 read and written,
-                  the catchment id (i32) and Qc (elem) when the variant reads
-                  them  (fp32 132 B, fp64 168 B)."""
+                  planes), state five f64 + window total i64 read and written,
+                  albedo (fp64 engine: f64 read and written; fp32 engine: f32
+                  written only -- the step rebuilds it from n and the depths,
+                  round 6), the catchment id (i32) and Qc (elem) when the
+                  variant reads them  (fp32 120 B, fp64 168 B)."""
     step = 5 * elem + 4 + 4 + 6 * elem
     geo = 5 * 4 if elem == 4 else 7 * 8
-    launch = geo + 2 * (6 * 8 + 8) + (4 if catchments else 0) + (elem if qc else 0)
+    albedo = 4 if elem == 4 else 2 * 8
+    launch = geo + 2 * (5 * 8 + 8) + albedo + (4 if catchments else 0) + (elem if qc else 0)
     return step, launch
 
 
 def launch_bytes_per_cell(fuse: int, elem: int = 4, catchments: bool = False, qc: bool = False) -> int:
     """Algorithmic HBM bytes per cell of one fused launch of `fuse` steps:
-    fp32 engine 52 per step + 132 per launch, fp64 engine 96 + 168.  (Keeping
+    fp32 engine 52 per step + 120 per launch, fp64 engine 96 + 168.  (Keeping
     the window slots that a launch reads back itself in LDS would save 8 B per
     such step, but reserving the LDS cost 8 % of throughput on its own: HISTORY.md.)"""
     step, launch = bytes_model(elem, catchments, qc)
@@ -643,7 +646,7 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
     update(), every step), with the inputs already on the device: per step
     one tfg_set_inputs from a device [5][n] f32 block (BMI order P_air, Hum_sp,
     P, T_air, uz: 20 B read + 20 B written per cell) and one tfg_step of one
-    step (a K = 1 launch: 52 + 132 = 184 B per cell-update).  Beside it the
+    step (a K = 1 launch: 52 + 120 = 172 B per cell-update).  Beside it the
     same steps queued: the inputs of `steps` steps set into as many frames,
     then one fused launch (what a deferred grid update() would do).  Never
     `value`."""
@@ -659,7 +662,7 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
                f"; queued: the same inputs into {steps} frames, then one {steps}-step launch" if args.dropin_queued
                else "")}
     # --dropin-clean: first the same K = 1 launches in the clean step form, for a same-run A/B of the two forms
-    # at 184 B per cell-update: the frames as fill_synthetic wrote them (known finite), no inputs set, each launch
+    # at 172 B per cell-update: the frames as fill_synthetic wrote them (known finite), no inputs set, each launch
     # between HIP events (before the per-step protocol, whose device-set inputs leave the frames of unknown
     # status).  Off by default: they are launches of the timed kernel instance at K = 1, which would enter its
     # rocprof average (profiles/r5_dropin_form_ab.json holds the A/B)

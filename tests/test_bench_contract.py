@@ -57,16 +57,18 @@ def test_driver_command_times_the_same_work_at_every_n(world, fuse):
 
 def test_byte_model_prices_each_engine_by_its_element_size():
     """roofline.achieved's algorithmic bytes: the fp32 engine 52 B per step +
-    132 B per launch (53.03 B per cell-update at the bench's 128-step
-    launches), the fp64 engine 96 + 168 (its forcing frames, output slots and
-    geometry are f64: 96.875 B at its automatic 192 steps on 4096^2)."""
+    120 B per launch (52.9375 B per cell-update at the bench's 128-step
+    launches; 172 B at one step per launch, the per-step drop-in path: the
+    albedo plane is written in fp32 and not read, round 6), the fp64 engine
+    96 + 168 (its forcing frames, output slots and geometry are f64: 96.875 B
+    at its automatic 192 steps on 4096^2)."""
     bench, _ = _args()
-    assert bench.bytes_model(4) == (52, 132) and bench.bytes_model(8) == (96, 168)
-    assert bench.launch_bytes_per_cell(128) / 128 == 53.03125
+    assert bench.bytes_model(4) == (52, 120) and bench.bytes_model(8) == (96, 168)
+    assert bench.launch_bytes_per_cell(128) / 128 == 52.9375 and bench.launch_bytes_per_cell(1) == 172
     k64 = bench.auto_fuse(4096 * 4096, 8)
     assert k64 == 192 and bench.launch_bytes_per_cell(k64, 8) / k64 == 96.875
     # the catchment variant reads the id raster, the conduction variant Qc, once per launch
-    assert bench.bytes_model(4, catchments=True, qc=True) == (52, 132 + 4 + 4)
+    assert bench.bytes_model(4, catchments=True, qc=True) == (52, 120 + 4 + 4)
 
 
 def test_pmc_traffic_is_keyed_by_engine_and_kernel_code(tmp_path, monkeypatch):

@@ -378,14 +378,15 @@ __global__ void k_convert(D* __restrict__ dst, const S* __restrict__ src, int64_
 
 // initialize() state (:389-395, :369, :288, :296) from the current depths
 __global__ void k_init_state(double* __restrict__ st, int64_t n_pad, double rhoCp_snow, double del_T,
-                             double Ecci0) {
+                             double Ecci0, int albedo_f32) {
 #pragma clang fp contract(off)
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
     const double e = rhoCp_snow * st[S_HSNOW * n_pad + i] * del_T;
     st[S_ECCS * n_pad + i] = tfg::npmax(e, 0.0);
     st[S_ECCI * n_pad + i] = Ecci0;
     st[S_N * n_pad + i] = 0.0;
-    st[S_ALB * n_pad + i] = 0.3;
+    if (albedo_f32) reinterpret_cast<float*>(st + S_ALB * n_pad)[i] = 0.3f;  // the fp32 engine's albedo plane
+    else st[S_ALB * n_pad + i] = 0.3;
   }
 }
 
@@ -918,7 +919,7 @@ void* field_ptr(tfg_handle* h, int field, int index, int* dtype) {
     case TFG_ST_CATCH_ID: *dtype = TFG_I32; return h->catch_id;
     case TFG_ST_ECCS: *dtype = TFG_F64; return h->st + S_ECCS * np;
     case TFG_ST_ECCI: *dtype = TFG_F64; return h->st + S_ECCI * np;
-    case TFG_ST_ALBEDO: *dtype = TFG_F64; return h->st + S_ALB * np;
+    case TFG_ST_ALBEDO: *dtype = h->engine == TFG_F32 ? TFG_F32 : TFG_F64; return h->st + S_ALB * np;  // fp32 engine: fp32
     case TFG_ST_NDAYS: *dtype = TFG_F64; return h->st + S_N * np;
     default: return nullptr;
   }
@@ -1404,7 +1405,8 @@ int tfg_init_state(tfg_handle* h) {
   const DevParams& p = h->dp;
   // Eccs = max((rho_snow*Cp_snow)*h_snow*del_T, 0); del_T = T0 - T_surf(=0)  (:389-395)
   const double del_T = p.T0 - 0.0;
-  hipLaunchKernelGGL(k_init_state, grid_for(h->n_pad), 256, 0, h->stream, h->st, h->n_pad, p.rho_snow_Cp_snow, del_T, p.Ecci0);
+  hipLaunchKernelGGL(k_init_state, grid_for(h->n_pad), 256, 0, h->stream, h->st, h->n_pad, p.rho_snow_Cp_snow, del_T, p.Ecci0,
+                     h->engine == TFG_F32 ? 1 : 0);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipMemsetAsync(h->tot, 0, (size_t)h->n_pad * 8, h->stream));
   HIPCHK(h, hipMemsetAsync(h->ring, 0, (size_t)h->ring_len * h->n_pad * 4, h->stream));
@@ -1467,7 +1469,24 @@ constexpr int kVerifySteps = 8;
 // (after prepare_steps has rebuilt them).  Synchronous.
 int check_state(tfg_handle* h) {
   uint8_t st = kOk;
-  if (int rc = check_finite(h, h->st, TFG_F64, h->n, &st, kNumState, h->n_pad)) return rc;
+  {  // the state planes, the albedo plane in the engine's type (fp32 for the fp32 engine)
+    const int64_t np = h->n_pad;
+    HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
+    hipLaunchKernelGGL((k_nonfinite<double>), grid_for(h->n), 256, 0, h->stream, (const double*)h->st, h->n, np, S_ALB, h->d_flag);
+    if (h->engine == TFG_F32)
+      hipLaunchKernelGGL((k_nonfinite<float>), grid_for(h->n), 256, 0, h->stream, (const float*)(h->st + S_ALB * np), h->n,
+                         (int64_t)0, 1, h->d_flag);
+    else
+      hipLaunchKernelGGL((k_nonfinite<double>), grid_for(h->n), 256, 0, h->stream, (const double*)(h->st + S_ALB * np), h->n,
+                         (int64_t)0, 1, h->d_flag);
+    hipLaunchKernelGGL((k_nonfinite<double>), grid_for(h->n), 256, 0, h->stream, (const double*)(h->st + (S_ALB + 1) * np),
+                       h->n, np, kNumState - S_ALB - 1, h->d_flag);
+    HIPCHK(h, hipGetLastError());
+    int32_t flag = 0;
+    HIPCHK(h, hipMemcpyAsync(&flag, h->d_flag, 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    st = flag ? kDirty : kOk;
+  }
   if (st == kOk) {
     HIPCHK(h, hipMemsetAsync(h->d_flag, 0, 4, h->stream));
     hipLaunchKernelGGL(k_window_nan, grid_for(h->n), 256, 0, h->stream, h->tot, h->n, h->d_flag);

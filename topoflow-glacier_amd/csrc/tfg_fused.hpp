@@ -29,7 +29,7 @@ constexpr int kCellsPerThread = 1;   // cells per lane (the streamed step access
 constexpr int kPrefetchFast = 2;     // time steps of forcing the fast engine requests ahead (HISTORY.md section 5)
 constexpr int kWaves = kBlock / 64;
 constexpr int kNumForc = 5;   // P, T_air, Hum_sp, P_air, uz  (device frame layout)
-constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo, h_snow, h_ice
+constexpr int kNumState = 8;  // h_swe, h_iwe, Eccs, Ecci, n, albedo (fp32 in the fp32 engine), h_snow, h_ice
 constexpr int kNumHist = 6;   // h_snow, SM, h_ice, IM, M_total, RH
 enum { S_HSWE = 0, S_HIWE, S_ECCS, S_ECCI, S_N, S_ALB, S_HSNOW, S_HICE };
 enum { F_P = 0, F_T, F_Q, F_PA, F_UZ };
@@ -262,9 +262,11 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
         dload<C>(st + S_N * n_pad, lc, v);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].n = v[j];
-        dload<C>(st + S_ALB * n_pad, lc, v);
+        if constexpr (EXACT) {
+          dload<C>(st + S_ALB * n_pad, lc, v);
 #pragma unroll
-        for (int j = 0; j < C; ++j) cs[j].albedo = v[j];
+          for (int j = 0; j < C; ++j) cs[j].albedo = v[j];
+        }
         if constexpr (READ_DEPTHS) {
           dload<C>(st + S_HSNOW * n_pad, lc, v);
 #pragma unroll
@@ -283,6 +285,26 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
         lload<C>(tot, lc, t);
 #pragma unroll
         for (int j = 0; j < C; ++j) cs[j].tot_q = t[j];
+        if constexpr (!EXACT) {
+          // The fp32 engine's albedo plane holds fp32 (round 6).  Albedo is
+          // rebuilt every step from n and the previous depths (:1041-1059);
+          // the stored value carries over only where those depths leave it
+          // (a NaN or negative snow depth, or no snow over a NaN or negative
+          // ice depth), so it is read only in a wave with such a lane: with
+          // the model's own depths the plane is written, never read.
+          bool carried = false;
+#pragma unroll
+          for (int j = 0; j < C; ++j) {
+            cs[j].albedo = 0.0;
+            carried |= !(cs[j].h_snow > 0.0 || (cs[j].h_snow == 0.0 && (cs[j].h_ice > 0.0 || cs[j].h_ice == 0.0)));
+          }
+          if (__any(carried)) {
+            float fa[C];
+            vload<float, C>(reinterpret_cast<const float*>(st + S_ALB * n_pad), lc, fa);
+#pragma unroll
+            for (int j = 0; j < C; ++j) cs[j].albedo = (double)fa[j];
+          }
+        }
       }
       // optional lateral conduction flux, held for the launch (tfg_conduction.hpp)
       R qc[C];
@@ -458,9 +480,16 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
 #pragma unroll
         for (int j = 0; j < C; ++j) v[j] = cs[j].n;
         dstore<C>(st + S_N * n_pad, lc, v);
+        if constexpr (EXACT) {
 #pragma unroll
-        for (int j = 0; j < C; ++j) v[j] = cs[j].albedo;
-        dstore<C>(st + S_ALB * n_pad, lc, v);
+          for (int j = 0; j < C; ++j) v[j] = cs[j].albedo;
+          dstore<C>(st + S_ALB * n_pad, lc, v);
+        } else {  // fp32 (the step computes it in fp32)
+          float fa[C];
+#pragma unroll
+          for (int j = 0; j < C; ++j) fa[j] = (float)cs[j].albedo;
+          vstore<float, C>(reinterpret_cast<float*>(st + S_ALB * n_pad), lc, fa);
+        }
         int64_t t[C];
 #pragma unroll
         for (int j = 0; j < C; ++j) t[j] = cs[j].tot_q;
