@@ -366,8 +366,10 @@ def capture_parity(eng, args, plan: dict, world: int, torch, local: int) -> dict
             return (x.sum() if how == "sum" else x.max()).reshape(1)
     da_dt = BASE_CFG["da"] * 1e6 * args.dt
     want = torch.stack([seg(sums[i], "sum") for i in range(3)], 1).cpu().numpy() * da_dt
+    # P_max starts at 0 (:314, the reference's initial value): a catchment with no cells in this shard (a
+    # rank's slab of the 43-catchment block raster holds only some of them) keeps 0
     return {"plan": pp, "gpu": gpu, "nan_safe_launches": ns, "diag": diag, "want_P_PR_PS": want,
-            "want_P_max": seg(pcell, "max").cpu().numpy()}
+            "want_P_max": np.maximum(seg(pcell, "max").cpu().numpy(), 0.0)}
 
 
 def oracle_sample(args, pp: dict, threads: int):

@@ -670,11 +670,6 @@ struct tfg_handle {
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
   bool force_ns = false;             // tfg_set_step_form(TFG_FORM_NAN_SAFE): every launch NaN-safe
   bool flux_f64 = false;             // tfg_set_flux(TFG_FLUX_F64): the fp32 engine's fp64-flux form
-  // a small grid's launches run as two halves on two streams (launch_steps):
-  // the second stream and the fork / join events, made on first use
-  hipStream_t side_stream = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  int resident_blocks = 0;           // k_fused workgroups resident on the device at once
   std::string err;
 };
 
@@ -937,16 +932,10 @@ struct IoArgs {
   uint8_t in_state = kUnknown;  // the inputs' finite-data status (tfg_handle::plane_state)
 };
 
-// One k_fused launch on `stream` over the chunks [chunk0, chunk0 + nchunks) of
-// kBlock cell groups (nchunks = 0: the whole plane stride), its workgroups
-// accumulating into the slab rows from slab_row0 on.
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns,
-                 hipStream_t stream, int chunk0 = 0, int nchunks = 0, int slab_row0 = 0) {
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns) {
+  const hipStream_t stream = h->stream;
   KArgs a;
-  a.chunk0 = chunk0;
-  a.nchunks = nchunks;
-  a.slab_row0 = slab_row0;
   a.p = h->dp;
   a.K = K;
   a.io_in = io.in;
@@ -1101,8 +1090,6 @@ int tfg_create(const tfg_params* p, int64_t ny, int64_t nx, int engine, int devi
   // section 5).  The per-workgroup diagnostic slab is kept under 256 MiB for
   // large catchment counts: 65536 workgroups at config 5's 43 catchments
   // (135 MB), +1.2 % on its slab against the 16384 a 64 MiB cap gave.
-  // k_fused runs 4 waves per SIMD (__launch_bounds__): 4 workgroups of kWaves waves per CU
-  h->resident_blocks = prop.multiProcessorCount * (4 * 4 / kWaves);
   h->max_blocks = std::max(256, prop.multiProcessorCount * 512);
   h->max_blocks = (int)std::max<int64_t>(256, std::min<int64_t>(h->max_blocks, (256ll << 20) / ((int64_t)n_catch * 6 * 8)));
   // a power of two: with many catchments a slab-capped odd count (31775 at 44
@@ -1162,12 +1149,6 @@ int tfg_destroy(tfg_handle* h) {
   if (h->out_d) (void)hipFree(h->out_d);
   if (h->out_h) (void)hipHostFree(h->out_h);
   if (h->io_h) (void)hipHostFree(h->io_h);
-  if (h->side_stream) {
-    (void)hipStreamSynchronize(h->side_stream);
-    (void)hipStreamDestroy(h->side_stream);
-  }
-  if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-  if (h->join_ev) (void)hipEventDestroy(h->join_ev);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
   delete h;
   return TFG_OK;
@@ -1561,29 +1542,6 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
   return TFG_OK;
 }
 
-// A launch of the fp32 engine as two halves of the cell groups, the first on
-// the handle's stream and the second on a side stream forked from and joined
-// back into it (stream order for the caller is unchanged); each half's
-// workgroups accumulate into their own slab rows, so the diagnostics stay
-// deterministic.
-int launch_split(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, bool ns) {
-  if (!h->side_stream) {
-    HIPCHK(h, hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
-    HIPCHK(h, hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-    HIPCHK(h, hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
-  }
-  const int chunks = (int)((h->n_pad / kCellsPerThread + kBlock - 1) / kBlock);  // <= 4 rounds of workgroups
-  const int c0 = chunks / 2;
-  const int b0 = blocks / 2, b1 = blocks - blocks / 2;
-  HIPCHK(h, hipEventRecord(h->fork_ev, h->stream));
-  HIPCHK(h, hipStreamWaitEvent(h->side_stream, h->fork_ev, 0));
-  if (int rc = launch_fused<float, false>(h, d_u, K, b0, lds, IoArgs(), ns, h->stream, 0, c0, 0)) return rc;
-  if (int rc = launch_fused<float, false>(h, d_u, K, b1, lds, IoArgs(), ns, h->side_stream, c0, chunks - c0, b0)) return rc;
-  HIPCHK(h, hipEventRecord(h->join_ev, h->side_stream));
-  HIPCHK(h, hipStreamWaitEvent(h->stream, h->join_ev, 0));
-  return TFG_OK;
-}
-
 int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
                  const IoArgs& io = IoArgs()) {
   if (int rc = prepare_steps(h)) return rc;
@@ -1594,15 +1552,6 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
   // (see the prefetch note in k_fused)
   const int fuse = h->ring_len > (h->engine == TFG_F32 ? kPrefetchFast : 1) ? h->fuse : 1;
   const bool one_cell = h->engine == TFG_F64 && h->n == 1 && !io.in;  // k_cell_run
-  // a grid of 2 to 4 rounds of resident workgroups (1024^2 cells on the
-  // MI355X: 4096 workgroups, 4 rounds of 1024) idles ~10 % of each launch in
-  // its drain; two half launches on two streams fill each other's drain
-  // (HISTORY.md section 10; fp32 engine, launches without tfg_update's host I/O)
-#ifndef TFG_SPLIT_SMALL  // measurement builds: -DTFG_SPLIT_SMALL=0 runs every grid as one launch
-#define TFG_SPLIT_SMALL 1
-#endif
-  const bool split = TFG_SPLIT_SMALL && h->engine == TFG_F32 && !io.in && blocks >= 2 * h->resident_blocks &&
-                     blocks <= 4 * h->resident_blocks;
   for (int64_t k0 = 0; k0 < nsteps; k0 += fuse) {
     const int K = (int)std::min<int64_t>(fuse, nsteps - k0);
     int rc = TFG_OK;
@@ -1625,14 +1574,14 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
     } else if (h->engine == TFG_F32) {
       bool ns = true;
       if ((rc = choose_form(h, u + k0, K, io, &ns))) return rc;
-      rc = split ? launch_split(h, d_u + k0, K, blocks, lds, ns) : launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, ns, h->stream);
+      rc = launch_fused<float, false>(h, d_u + k0, K, blocks, lds, io, ns);
       if (ns) {
         ++h->ns_launches;
         // the NaN-safe form may have carried missing data into the state
         if (h->state_state == kOk) h->state_state = kUnknown;
       }
     } else {
-      rc = launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, false, h->stream);
+      rc = launch_fused<double, true>(h, d_u + k0, K, blocks, lds, io, false);
     }
     if (rc) return rc;
     h->depths_derived = true;

@@ -52,11 +52,6 @@ struct KArgs {
   double* io_out;
   uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
   uint32_t io_seq;
-  // the chunks of kBlock cell groups this launch steps, [chunk0, chunk0 +
-  // nchunks) (nchunks = 0: the whole plane stride), and its first slab row: a
-  // small grid runs as two such launches on two streams (launch_split)
-  int chunk0 = 0, nchunks = 0;
-  int slab_row0 = 0;
 };
 
 // TFG_STEP_PARAMS(p): inside a step loop, `p` names the launch's model
@@ -202,10 +197,10 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
-  const int64_t nchunks = a.nchunks > 0 ? a.nchunks : (ngroups + kBlock - 1) / kBlock;
+  const int64_t nchunks = (ngroups + kBlock - 1) / kBlock;
   const int64_t wg = blockIdx.x;
-  const int64_t g0 = (a.chunk0 + wg * nchunks / gridDim.x) * kBlock;
-  const int64_t g1 = std::min<int64_t>((a.chunk0 + (wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
+  const int64_t g0 = (wg * nchunks / gridDim.x) * kBlock;
+  const int64_t g1 = std::min<int64_t>(((wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
   const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad);
 
@@ -505,7 +500,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
   __syncthreads();
   // each workgroup accumulates into its own slab row across launches (fixed
   // order, deterministic); tfg_get_diag folds the rows when it is called
-  double* bslab = slab + ((int64_t)blockIdx.x + a.slab_row0) * nb;
+  double* bslab = slab + (int64_t)blockIdx.x * nb;
   for (int i = threadIdx.x; i < nb; i += kBlock) {
     double v = lds_bins[i];
     if ((i % 6) == 5) {
