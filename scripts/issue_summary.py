@@ -17,6 +17,8 @@ res = {}
 # parity or drop-in legs, so every dispatch of these is a whole `fuse`-step launch
 F32_FUSE, F64_FUSE = (int(a) for a in (sys.argv[2:4] if len(sys.argv) > 3 else (128, 192)))
 for name, kern, cells, fuse in (("f32", "k_fused<float, false, false, false, false, 1, false, false>", 8192 * 8192, F32_FUSE),
+                                ("f32_flux_f64", "k_fused<float, false, false, false, false, 1, false, true>", 8192 * 8192,
+                                 F32_FUSE),
                                 ("f64", "k_fused<double, true, false, false, false, 1, false, false>", 4096 * 4096, F64_FUSE)):
     raw = defaultdict(list)
     for f in sorted(glob.glob(f"{d}/{name}/p*/run_counter_collection.csv")):

@@ -143,11 +143,12 @@ def flux(variant, K, u, elev, geo, T, Q, PA, uz, h_snow, h_ice, albedo, n_days):
     else:
         bot = (uz * uz) * T_K
         bot = np.where(bot == 0, f32(0.01), bot)
-        Ri = f32(K.gz) * dTs * hw_rcp(bot)
+        rcp = rcp_nr32 if "rcpnr" in v else hw_rcp  # "rcpnr": Newton-refined reciprocals in Ri, Dn, Dh
+        Ri = f32(K.gz) * dTs * rcp(bot)
         ly2 = hw_log2(np.maximum((f32(10.0) - h_snow.astype(f32)) * f32(K.inv_z0s), f32(K.l2min)))
         L2sq = fma32(ly2, ly2 + f32(2 * K.k), f32(K.k * K.k))
-        Dn = uz * f32(K.k2) * hw_rcp(L2sq)
-        Dh32 = np.where(Ri > 0, Dn * hw_rcp(fma32(f32(10), Ri, f32(1))), Dn * fma32(f32(-10), Ri, f32(1)))
+        Dn = uz * f32(K.k2) * rcp(L2sq)
+        Dh32 = np.where(Ri > 0, Dn * rcp(fma32(f32(10), Ri, f32(1))), Dn * fma32(f32(-10), Ri, f32(1)))
         Dh = f64(Dh32)
         Qh = f64(f32(K.rhoCp) * Dh32 * dTs)
     # latent
