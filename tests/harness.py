@@ -345,12 +345,23 @@ def classify_sample(gpu: dict, ref: dict, c64: dict, cfg: dict, tol: float, onse
                            onset_ok=len(onset) <= int(np.ceil(ONSET_FRAC_MAX * ncell)))
 
 
+# "float32-fluxf64": the fp32 engine's fp64-flux form (tfg_set_flux), as a third engine name of the tests
+FLUX_F64_ENGINE = "float32-fluxf64"
+
+
+def split_engine(engine: str) -> tuple[str, str]:
+    """(engine, flux) of a test engine name."""
+    return ("float32", "fp64") if engine == FLUX_F64_ENGINE else (engine, "fp32")
+
+
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
                 fuse_steps: int = 24, row0: int = 0, flux: str = "fp32"):
     from topoflow_glacier.engine import GlacierEngine
 
+    engine, f = split_engine(engine)
     return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
-                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0, flux=flux)
+                         hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0,
+                         flux=f if f == "fp64" else flux)
 
 
 def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,
@@ -519,11 +530,12 @@ def run_gpu_vs_oracle(ny: int, nx: int, nsteps: int, engine: str = "float32", se
     report = {}
     worst = 0.0
     worst_rel = 0.0
-    tol = 1e-5 if engine == "float32" else 1e-10
-    excused = depletion_steps(gpu, ref, cfg, tol, OUT_EPS_F32 if engine == "float32" else OUT_EPS_F64)
+    fp32 = split_engine(engine)[0] == "float32"
+    tol = 1e-5 if fp32 else 1e-10
+    excused = depletion_steps(gpu, ref, cfg, tol, OUT_EPS_F32 if fp32 else OUT_EPS_F64)
     flip, genuine = melt_out_flips(gpu, ref, tol, excused)
     onset = {}
-    # TFG_STRICT_ONSET=1: no onset allowance (to list the tests that need it)
+    # TFG_STRICT_ONSET=1: no onset allowance (to list the tests that need it); never for the fp64 flux
     if engine == "float32" and genuine and os.environ.get("TFG_STRICT_ONSET") != "1":
         onset, genuine = melt_onsets(gpu, ref, genuine, cfg)
     cut = flip.copy()

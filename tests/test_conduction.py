@@ -17,8 +17,8 @@ adds Qc last, :1314) and leaves it at zero.  Two things are checked:
 import numpy as np
 import pytest
 
-from tests.harness import (BASE_CFG, RestatedCondShard, conduction_cells, conduction_restated, conduction_state,
-                           make_engine, run_gpu_vs_oracle)
+from tests.harness import (BASE_CFG, FLUX_F64_ENGINE, RestatedCondShard, conduction_cells, conduction_restated,
+                           conduction_state, make_engine, run_gpu_vs_oracle, split_engine)
 from tests.test_sharding import _torchrun
 from topoflow_glacier.sharding import lateral_conduction, row_block
 
@@ -95,7 +95,7 @@ def _engine(st, engine="float32", row0=0):
 
 
 def _as_engine(qc, engine):
-    return qc.astype(np.float32).astype(np.float64) if engine == "float32" else qc
+    return qc.astype(np.float32).astype(np.float64) if split_engine(engine)[0] == "float32" else qc
 
 
 def _halos(full, lo, hi):
@@ -168,7 +168,7 @@ def _cold(ny, nx, seed=5):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("engine", ["float32", "float64"])
+@pytest.mark.parametrize("engine", ["float32", "float64", FLUX_F64_ENGINE])
 def test_gpu_fixed_qc_enters_q_sum_like_the_reference(engine):
     """A given Qc field (set as TFG_ST_QC) enters Q_sum where the reference
     adds its Qc (:1314): the engine matches the oracle run with the same Qc,

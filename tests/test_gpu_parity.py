@@ -21,9 +21,9 @@ import pandas as pd
 import pytest
 import yaml
 
-from tests.harness import (BASE_CFG, GOLDEN, OUT_NAMES, c_oracle_hist, flip_rule, fp64_baseline_flips, gpu_run_fields,
-                           load_golden, make_engine, melt_out_flips, oracle_run, parity, run_gpu_vs_oracle,
-                           synthetic_inputs, valid_mask)
+from tests.harness import (BASE_CFG, FLUX_F64_ENGINE, GOLDEN, OUT_NAMES, c_oracle_hist, flip_rule, fp64_baseline_flips,
+                           gpu_run_fields, load_golden, make_engine, melt_out_flips, oracle_run, parity,
+                           run_gpu_vs_oracle, split_engine, synthetic_inputs, valid_mask)
 
 pytestmark = pytest.mark.gpu
 HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
@@ -212,6 +212,15 @@ def test_fp32_engine_vs_oracle_on_fixture_inputs(name):
 def test_fp32_synthetic_vs_oracle(shape, nsteps):
     rep = run_gpu_vs_oracle(shape[0], shape[1], nsteps, "float32", seed=11)
     assert rep["ok"], rep["summary"]
+
+
+@pytest.mark.parametrize("shape,nsteps", [((32, 64), 48), ((3, 65), 30)])
+def test_flux_fp64_synthetic_vs_oracle(shape, nsteps):
+    """The fp32 engine's fp64-flux form (tfg_set_flux(TFG_FLUX_F64)) on the
+    synthetic workload: the floored 1e-5 with no melt-onset allowance."""
+    rep = run_gpu_vs_oracle(shape[0], shape[1], nsteps, FLUX_F64_ENGINE, seed=11)
+    assert rep["ok"] and not rep["onsets"], rep["summary"]
+    assert rep["max_rel"] <= 2e-6, rep["summary"]
 
 
 def test_fp64_synthetic_vs_oracle():
@@ -670,7 +679,7 @@ def _report(name, obj):
             json.dump(obj, f, indent=1)
 
 
-@pytest.mark.parametrize("engine", ["float64", "float32"])
+@pytest.mark.parametrize("engine", ["float64", "float32", FLUX_F64_ENGINE])
 def test_engine_propagates_nan_forcing_like_the_reference(engine):
     """Missing forcing (NaN) takes the same path as in the reference's numpy
     arithmetic, in both engines: np.maximum / np.minimum propagate NaN
@@ -685,7 +694,8 @@ def test_engine_propagates_nan_forcing_like_the_reference(engine):
     g = load_golden("grid64")
     cells = slice(8, 16)
     nsteps = 100  # past step 5 + 72: the NaN slot leaves the window and n runs again
-    r32 = (lambda a: np.asarray(a, np.float32).astype(np.float64)) if engine == "float32" else np.asarray  # noqa: E731
+    fp32 = split_engine(engine)[0] == "float32"  # both flux forms of the fp32 engine
+    r32 = (lambda a: np.asarray(a, np.float32).astype(np.float64)) if fp32 else np.asarray  # noqa: E731
     forcing = {k: np.array(r32(v[:nsteps, cells]), copy=True) for k, v in g["forcing"].items()}
     static = {k: r32(v[cells]) for k, v in g["static"].items()}
     forcing["T_air"][3, 0] = np.nan
@@ -698,7 +708,7 @@ def test_engine_propagates_nan_forcing_like_the_reference(engine):
     ref, m = oracle_run(g["cfg"], static, forcing)
     assert np.isnan(ref["M_total"][-1, :5]).all() and np.isfinite(ref["M_total"][-1, 5:]).all()
     assert abs(m.n[1] * 86400.0 - (nsteps - 72)) < 1e-6  # cell 1's n froze while its NaN slot was in the window
-    if engine == "float64":
+    if not fp32:
         ok_steps = np.ones((nsteps, 8), dtype=bool)
     else:
         flip, genuine = melt_out_flips(outs, ref, 1e-5)
@@ -708,7 +718,7 @@ def test_engine_propagates_nan_forcing_like_the_reference(engine):
     for v in HIST:
         np.testing.assert_array_equal(np.isnan(outs[v]), np.isnan(ref[v]), err_msg=v)
         ok = ~np.isnan(ref[v]) & ok_steps
-        if engine == "float64":
+        if not fp32:
             assert _rel(outs[v][ok], ref[v][ok]) <= 1e-10, v
         else:
             assert parity(outs[v], np.where(np.isnan(ref[v]), 0.0, ref[v]), mask=ok)[0] <= 1e-5, v
@@ -717,7 +727,7 @@ def test_engine_propagates_nan_forcing_like_the_reference(engine):
         want = np.asarray(getattr(m, v), np.float64)
         np.testing.assert_array_equal(np.isnan(state[v]), np.isnan(want), err_msg=v)
         fin = np.isfinite(want) & keep
-        tol = 1e-10 if engine == "float64" else 1e-5
+        tol = 1e-10 if not fp32 else 1e-5
         assert parity(state[v], want, mask=fin)[0] <= tol, (v, state[v], want)
     assert state["n"][1] == m.n[1]  # frozen over the 72 steps the NaN slot spent in the window
     np.testing.assert_array_equal(np.isnan(diag[0, :5]), np.isnan([m.vol_P, m.vol_PR, m.vol_PS, m.vol_SM, m.vol_IM]))
