@@ -178,7 +178,7 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert d["ranks"]["ranks"][0]["sample_parity"]["ok"]
     # the drop-in legs: per-step K = 1 launches from device inputs, and queued steps; defer_update instances
     g = d["dropin_per_step_grid"]
-    assert g["per_step"]["value"] > 0 and g["queued"]["value"] > 0 and g["per_step"]["bytes_per_cell_update"] == 184
+    assert g["per_step"]["value"] > 0 and g["queued"]["value"] > 0 and g["per_step"]["bytes_per_cell_update"] == 172
     # the same-run A/B of the step forms at K = 1: device-set inputs run NaN-safe, host-checked frames clean
     assert g["per_step"]["nan_safe_launches"] == 24 and g["clean_form_step_launch"]["nan_safe_launches"] == 0
     assert g["clean_form_step_launch"]["nan_safe_over_clean"] > 0
