@@ -2,8 +2,8 @@
 # smoke().  PART=p -- the fp32 PMC traffic profile (installed as profiles/pmc_8192x8192_fuse128.json for
 # the bench to quote), rocprofv3 kernel-trace stats of the driver's bench command and the driver / no-flag
 # bench lines (scripts/gpu_prof.sh).  PART=b -- the fp64 engine's PMC profile and bench line, the issue counters of
-# both engines and the fp64-flux form, the fp64-flux bench line (with its parity check) and every
-# BASELINE configuration's line (scripts/gpu_baseline_configs.sh).
+# both engines and the fp64-flux form, the fp64-flux bench line (with its parity check).  PART=c -- every
+# BASELINE configuration's line (scripts/gpu_baseline_configs.sh) and the N > 1 rehearsal on one GPU.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -25,6 +25,14 @@ if [ "$PART" = p ]; then
   TAG=$TAG bash scripts/gpu_prof.sh
   exit $?
 fi
+if [ "$PART" = c ]; then
+  echo "== configurations"
+  bash scripts/gpu_baseline_configs.sh
+  rc=$?; [ $rc -eq 0 ] || exit $rc
+  echo "== N > 1 rehearsal (gloo, every rank on cuda:0)"
+  TAG=$TAG/reh bash scripts/gpu_r5_rehearse.sh
+  exit $?
+fi
 PMC_TAG=$TAG/pmc64 PMC_ENGINE=float64 PMC_SHAPE="4096 4096 192" \
   PMC_ARGS="--engine float64 --ny 4096 --nx 4096 --fuse 192 --steps 768 --warmup 192 --no-cpu-baseline --no-dropin --no-parity" \
   PMC_PROFILE=gpurun_out/$TAG/pmc_4096x4096_fuse192_f64.json bash scripts/gpu_pmc.sh || exit $?
@@ -40,5 +48,4 @@ rc=$?; echo "bench flux f64 rc=$rc"; grep '^{' gpurun_out/$TAG/bench_flux_f64.lo
 echo "== issue counters"
 TAG=$TAG/issue bash scripts/gpu_pmc_issue.sh > gpurun_out/$TAG/issue.log 2>&1 || { tail -5 gpurun_out/$TAG/issue.log; exit 1; }
 grep -c pass gpurun_out/$TAG/issue.log
-echo "== configurations"
-bash scripts/gpu_baseline_configs.sh
+exit 0

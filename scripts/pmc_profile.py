@@ -77,9 +77,9 @@ def calibration(d: Path, cells: int, steps: int):
 
 
 KERNELS = {  # engine -> (rocprofv3 kernel-name match, _native symbol prefix, description)
-    "float32": ("k_fused<float, false, false", "BENCH_KERNEL", "k_fused<float,false,false,false,false,1,false> (fp32 engine, clean form"),
+    "float32": ("k_fused<float, false, false", "BENCH_KERNEL", "k_fused<float,false,false,false,false,1,false,false> (fp32 engine, clean form"),
     "float64": ("k_fused<double, true, false, false, false", "BENCH_KERNEL_F64",
-                "k_fused<double,true,false,false,false,1,false> (fp64 engine"),
+                "k_fused<double,true,false,false,false,1,false,false> (fp64 engine"),
 }
 
 
