@@ -116,6 +116,16 @@ template <int C> __device__ __forceinline__ void istore(int32_t* p, uint32_t i, 
 template <int C> __device__ __forceinline__ void lload(const int64_t* p, uint32_t i, int64_t (&v)[C]) { vload<int64_t, C>(p, i, v); }
 template <int C> __device__ __forceinline__ void lstore(int64_t* p, uint32_t i, const int64_t (&v)[C]) { vstore<int64_t, C>(p, i, v); }
 
+// the fp64 step's unscaled sums (cell_step_exact, melt_and_mass<true>) times the
+// constant factors of :567, :585-623 (da dt) and :1486, :1493 (da dt 3600)
+__device__ __forceinline__ void diag_scale(CellDiag& d, const DevParams& p) {
+  const double f = p.da_m2 * p.dt, f3600 = p.da_m2 * p.dt * 3600.0;
+  d.P *= f;
+  d.PR *= f;
+  d.PS *= f;
+  d.SM *= f3600;
+  d.IM *= f3600;
+}
 __device__ __forceinline__ void diag_zero(CellDiag& d) {
   d.P = d.PR = d.PS = d.SM = d.IM = 0.0;
   d.Pmax = -INFINITY;
@@ -488,9 +498,13 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
     }
     if constexpr (CATCH) {
 #pragma unroll
-      for (int j = 0; j < C; ++j) wave_flush(wbins, cid[j], cacc[j], in);
+      for (int j = 0; j < C; ++j) {
+        if constexpr (EXACT) diag_scale(cacc[j], p);
+        wave_flush(wbins, cid[j], cacc[j], in);
+      }
     }
   }
+  if constexpr (EXACT && !CATCH) diag_scale(acc, p);
   if constexpr (!CATCH) wave_flush(wbins, 0, acc, true);
   __syncthreads();
   // each workgroup accumulates into its own slab row across launches (fixed

@@ -263,6 +263,9 @@ __device__ __forceinline__ bool sun_down(const DevParams& p, const CellStatic& s
 // State update after the net energy flux (fp64, reference order).
 // :1566-1731 -- shared by both variants.
 // ---------------------------------------------------------------------------
+// RAW (the grid kernel, round 6): the diagnostics gather SM and IM unscaled;
+// k_fused applies da dt 3600 to the launch's sums (diag_scale).
+template <bool RAW = false>
 __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, double P_snow,
                                               double P_rain, double RH, double T_wb,
                                               CellState& st, CellOut& o,
@@ -276,9 +279,14 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   double SM = div_r(div_r(E_rem, p.inv_dt), p.inv_rho_H2O_Lf);
   // enforce_max_snow_meltrate :1447-1465 -- only max(SM,0) executes; the
   // min(SM, h_swe/dt) lines are inside the method's docstring.
-  SM = npmax(SM, 0.0);
+  // an identity where 1/dt and 1/(rho_H2O Lf) are > 0 (E_rem >= 0 or NaN): skipped there (round 6)
+  const bool scale_pos = p.inv_dt > 0.0 && p.inv_rho_H2O_Lf > 0.0;
+  if (!scale_pos) SM = npmax(SM, 0.0);
   // update_SM_integral :1486
-  if (valid) d.SM += SM * p.da_m2 * dt * 3600.0;
+  if (valid) {
+    if constexpr (RAW) d.SM += SM;
+    else d.SM += SM * p.da_m2 * dt * 3600.0;
+  }
   // update_swe :1594-1606
   double h_swe = st.h_swe + P_snow * dt;
   double t = npmin(SM * 3600.0, h_swe);
@@ -295,7 +303,7 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   // update_ice_meltrate :1418-1434
   E_rem = npmax(E_in - st.Ecci, 0.0);
   double IM = div_r(div_r(E_rem, p.inv_dt), p.inv_rho_H2O_Lf);
-  IM = npmax(IM, 0.0);
+  if (!scale_pos) IM = npmax(IM, 0.0);
   IM = (h_swe == 0.0 && previous_swe == 0.0) ? IM : 0.0;
   double Ecci = npmax(st.Ecci - E_in, 0.0);
   Ecci = (st.h_ice == 0.0) ? 0.0 : Ecci;  // previous-step h_ice
@@ -303,7 +311,10 @@ __device__ __forceinline__ void melt_and_mass(const DevParams& p, double Q_sum, 
   IM = npmin(IM, div_k(st.h_iwe, dt, p.inv_dt));
   IM = npmax(IM, 0.0);
   // update_IM_integral :1493
-  if (valid) d.IM += IM * p.da_m2 * dt * 3600.0;
+  if (valid) {
+    if constexpr (RAW) d.IM += IM;
+    else d.IM += IM * p.da_m2 * dt * 3600.0;
+  }
   // update_iwe :1612-1617
   t = npmin(IM * 3600.0, st.h_iwe);
   IM = div_k(t, 3600.0, 1.0 / 3600.0);
@@ -512,11 +523,11 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
   // :567, :576, :585, :604, :613, :623
   const double P_rain = P * ((T_air > p.T_rs) ? 1.0 : 0.0);
   const double P_snow = P * ((T_air <= p.T_rs) ? 1.0 : 0.0);
-  if (valid) {
-    d.P += P * p.da_m2 * dt;
+  if (valid) {  // unscaled: k_fused applies da dt to the launch's sums (diag_scale; round 6)
+    d.P += P;
     d.Pmax = npmax(d.Pmax, P);
-    d.PR += P_rain * p.da_m2 * dt;
-    d.PS += P_snow * p.da_m2 * dt;
+    d.PR += P_rain;
+    d.PS += P_snow;
   }
   // :817-826
   double e = fdiv(Hum_sp * P_air, p.eps + (p.one_minus_eps * Hum_sp));
@@ -618,7 +629,7 @@ __device__ inline void cell_step_exact(const DevParams& p, const CellStatic& s, 
     T_wb = wet_bulb_finish(T_air, RH, at0, atan_q(num, den), den, at_small);
   }
   const DevParams& p4 = params();  // melt and mass phase
-  melt_and_mass(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
+  melt_and_mass<true>(p4, Q_sum, P_snow, P_rain, RH, T_wb, st, o, d, valid);
 #if defined(TFG_DEBUG_EXACT)  // diagnostic builds only: a flux term replaces RH in the output
   { const double dbg[8] = {Q_sum, Qn_SW, Qn_LW, Qh, Qe, K_cs, LW_in, albedo}; o.RH = dbg[TFG_DEBUG_EXACT]; }
 #endif
