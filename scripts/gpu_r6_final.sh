@@ -30,7 +30,7 @@ if [ "$PART" = c ]; then
   bash scripts/gpu_baseline_configs.sh
   rc=$?; [ $rc -eq 0 ] || exit $rc
   echo "== N > 1 rehearsal (gloo, every rank on cuda:0)"
-  TAG=$TAG/reh bash scripts/gpu_r5_rehearse.sh
+  TAG=$TAG/reh bash scripts/gpu_rehearse.sh
   exit $?
 fi
 PMC_TAG=$TAG/pmc64 PMC_ENGINE=float64 PMC_SHAPE="4096 4096 192" \
