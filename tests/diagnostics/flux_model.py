@@ -27,6 +27,7 @@ ROOT = Path(__file__).resolve().parents[2]
 sys.path[:0] = [str(ROOT / "topoflow-glacier_amd"), str(ROOT / "oracle"), str(ROOT)]
 
 f32, f64 = np.float32, np.float64
+NF = 24  # forcing frames (the year test: 24, repeated daily; 8760: no repetition)
 LOG2E = 1.4426950408889634
 LN2 = 0.6931471805599453
 
@@ -45,9 +46,14 @@ def fma32(a, b, c):
     return (np.asarray(a, f64) * np.asarray(b, f64) + np.asarray(c, f64)).astype(f32)
 
 
+IDEAL = bool(int(__import__("os").environ.get("TFG_FM_IDEAL", "0")))  # correctly rounded hardware functions
+
+
 def hw_exp2(x):
     x = np.asarray(x, f32)
     y = np.exp2(x.astype(f64))
+    if IDEAL:
+        return y.astype(f32)
     return (y * (1.0 + 1.7e-7 * _hash_u(x, 1))).astype(f32)
 
 
@@ -56,12 +62,16 @@ def hw_log2(x):
     with np.errstate(divide="ignore", invalid="ignore"):
         y = np.log2(x.astype(f64))
         yr = y.astype(f32)
+        if IDEAL:
+            return yr
         ulp = np.spacing(np.abs(yr)).astype(f64)
         return (y + ulp * (-0.44 + 0.5 * _hash_u(x, 2))).astype(f32)
 
 
 def hw_rcp(x):
     x = np.asarray(x, f32)
+    if IDEAL:
+        return (1.0 / x.astype(f64)).astype(f32)
     return ((1.0 / x.astype(f64)) * (1.0 + 1.0e-7 * _hash_u(x, 3))).astype(f32)
 
 
@@ -211,12 +221,12 @@ def flux(variant, K, u, elev, geo, T, Q, PA, uz, h_snow, h_ice, albedo, n_days):
     return Qs, {"Qn_SW": Qsw, "Qn_LW": Qlw, "Qh": Qh, "Qe": Qe}
 
 
-def setup(n=2048, seed=20251001):
+def setup(n=2048, seed=20251001, nf=None):
     import tfg_oracle as O
     from tests.harness import BASE_CFG, synthetic_inputs
     from topoflow_glacier.physics.clock import StepClock
 
-    syn, d = synthetic_inputs(seed, 1, n, 24)
+    syn, d = synthetic_inputs(seed, 1, n, nf or NF)
     static = {k: np.asarray(syn[s], f64) for k, s in (("elev", "elev"), ("slope", "slope"), ("aspect", "aspect"),
               ("h0_snow", "h_snow"), ("h0_ice", "h_ice"), ("h0_swe", "h_swe"), ("h0_iwe", "h_iwe"))}
     cfg = dict(BASE_CFG)
@@ -250,7 +260,7 @@ def one_step_errors(variants, steps=8760, n=2048):
     err = {v: np.empty((steps, n), f32) for v in variants}
     terms = {v: {t: np.zeros(n) for t in ("Qn_SW", "Qn_LW", "Qh", "Qe")} for v in variants}
     for k in range(steps):
-        f = k % 24
+        f = k % NF
         hs, hi = m.h_snow.copy(), m.h_ice.copy()
         r = m.step(*(F[x][f] for x in F), jd[k], tsn[k])
         u = {name: U[name][k] for name in U.dtype.names}
@@ -284,7 +294,7 @@ def year_metrics(dq, n=2048, steps=8760):
         for k in range(steps):
             if d is not None:
                 m.Qc = f64(d[k])
-            r = m.step(*(F[x][k % 24] for x in F), jd[k], tsn[k])
+            r = m.step(*(F[x][k % NF] for x in F), jd[k], tsn[k])
             runoff += r["M_total"] * 3600.0
             if k % 24 == 23:
                 for v in HIST:
@@ -311,7 +321,9 @@ def year_metrics(dq, n=2048, steps=8760):
 
 
 if __name__ == "__main__":
-    variants = sys.argv[1:] or ["base"]
+    args = [a for a in sys.argv[1:] if not a.startswith("--frames=")]
+    NF = int(next((a.split("=")[1] for a in sys.argv[1:] if a.startswith("--frames=")), NF))
+    variants = args or ["base"]
     steps = 8760
     err, rms = one_step_errors(variants, steps)
     print(json.dumps(rms, indent=1), flush=True)

@@ -16,6 +16,9 @@ extern "C" void fm_eval(const double* x, double* y, long n, int which) {
       case 11: y[i] = tfg_fm::fdiv(7.3, v); break;
       case 12: y[i] = tfg_fm::atan_q(v, 7.3); break;
       case 13: y[i] = tfg_fm::atan_q(-7.3, v); break;
+      case 14: y[i] = tfg_fm::exp_p(v); break;
+      case 15: y[i] = tfg_fm::log_p(v); break;
+      case 16: y[i] = tfg_fm::exp_near(v); break;
       default: y[i] = 0.0; break;
     }
   }

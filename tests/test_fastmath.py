@@ -31,6 +31,7 @@ SRC = ROOT / "tests" / "native" / "fastmath_host.cpp"
 HEADER = ROOT / "topoflow-glacier_amd" / "csrc" / "tfg_fastmath.hpp"
 EXP, EXP_LIBM, LOG, LOG_LIBM, DIV_61121, DIV_3600, EXP_VGPR, FDIV_BY_73, FDIV_73_BY = 3, 4, 5, 6, 7, 8, 9, 10, 11
 ATAN_BY_73, ATAN_M73_BY = 12, 13
+EXP_P, LOG_P, EXP_NEAR = 14, 15, 16  # the fp32 engine's fp64-flux form (round 6)
 
 # the bounds HISTORY.md section 5 states (ulps of numpy's result)
 EXP_ULPS = 3.0  # degree-10 polynomial since round 5 (the device libm's degree 12: 1 ulp)
@@ -183,6 +184,35 @@ def test_log_within_four_absolute_ulp_of_numpy(host):
         fin = np.isfinite(want) & (SPECIAL != 1.0)
         assert _same(ev(SPECIAL, LOG)[~fin], want[~fin])  # 0, -0, inf, -inf, NaN, negatives, log(1) = 0
         assert _log_err(ev(SPECIAL, LOG)[fin], want[fin]).max() <= LOG_ULPS
+
+
+def test_flux_form_exp_and_log_within_their_stated_bounds(host):
+    """The fp64-flux form's exp_p (degree 7, 5.2e-11 relative), exp_near
+    (exp(c + s) / exp(c) for |s| <= 0.41 without reduction, 5.1e-12) and log_p
+    (log_k on exp_p, ~6e-11 absolute): sized for the ~1e-9 the flux form needs
+    (DESIGN.md section 3), each held with a factor-2 margin on its fit's bound
+    plus the fp64 evaluation's rounding, over the physics' arguments; the special
+    values as exp_k / log_k."""
+    ev, _ = host
+    rng = np.random.default_rng(17)
+    for name, x in zip(("physics", "finite range"), exp_arguments(rng)):
+        ref = np.exp(x)
+        ok = (ref > 1e-300) & (ref < 1e300)
+        rel = np.abs(ev(x, EXP_P)[ok] - ref[ok]) / ref[ok]
+        assert rel.max() <= 1.1e-10, (name, float(rel.max()))
+    with np.errstate(over="ignore", under="ignore", invalid="ignore"):
+        assert _same(ev(SPECIAL[[2, 3, 4, 0, 1, 11, 10]], EXP_P), np.exp(SPECIAL[[2, 3, 4, 0, 1, 11, 10]]))
+    s = np.concatenate([rng.uniform(-0.41, 0.41, 200000), [-0.41, 0.0, 0.41]])
+    rel = np.abs(ev(s, EXP_NEAR) - np.exp(s)) / np.exp(s)
+    assert rel.max() <= 1.2e-11, float(rel.max())
+    # the dew point's argument e_air / 6.1121 (e_air ~0.01-80 mbar) and a wide positive range
+    for x in (np.exp(rng.uniform(np.log(1e-3), np.log(15.0), 200000)), np.exp(rng.uniform(-80.0, 80.0, 200000))):
+        err = np.abs(ev(x, LOG_P) - np.log(x))
+        assert (err / np.maximum(np.abs(np.log(x)), 1.0)).max() <= 1.5e-10, float(err.max())
+    with np.errstate(divide="ignore", invalid="ignore"):
+        want = np.log(SPECIAL)
+        fin = np.isfinite(want)
+        assert _same(ev(SPECIAL, LOG_P)[~fin], want[~fin])
 
 
 def _atan_exact(n, d):

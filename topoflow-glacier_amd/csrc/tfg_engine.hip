@@ -882,7 +882,8 @@ void derive_params(const tfg_params& q, DevParams& p) {
   p.d_k2 = (q.kappa / std::log(2.0)) * (q.kappa / std::log(2.0));
   p.d_l2k = (double)p.f_l2k2 * 0.5;
   p.d_l2kk = (double)p.f_l2kk;
-  p.d_qe = p.rho_air_Lv * q.latent_heat_constant * 100.0 / q.sea_level_p0;
+  // exp(c) of the flux form's lhc / p0 = exp(c) exp(y - c) (tfg_fm::exp_near)
+  p.d_qe = p.rho_air_Lv * q.latent_heat_constant * 100.0 / q.sea_level_p0 * std::exp(tfg_fm::kP0Center);
   p.d_es_k = q.satterlund ? 2353.0 * std::log(10.0) : 17.3 * 237.3;
   p.d_es_c = q.satterlund ? 273.15 : 237.3;
 }

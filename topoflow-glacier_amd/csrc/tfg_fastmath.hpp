@@ -173,6 +173,58 @@ TFG_FM_HD inline double exp_k(double x) { return exp_impl<true>(x); }
 TFG_FM_HD inline double exp_kv(double x) { return exp_impl<false>(x); }
 
 // ---------------------------------------------------------------------------
+// exp sized for the fp32 engine's fp64-flux form (round 6): that form needs its
+// flux terms within ~1e-9 (a per-step error of 2e-8 of the
+// flux magnitudes is what the year-long run tolerates), not exp_k's 3 ulp.
+// One-constant Cody-Waite reduction (|dn ln2_lo| < 1e-13 for |x| <= 708) and a
+// degree-7 polynomial (scripts/fit_exp.py 7: 5.2e-11 relative): 4 VALU fewer.
+// ---------------------------------------------------------------------------
+TFG_FM_HD inline double exp_p(double x) {
+  TFG_FM_NO_CONTRACT
+  const double dn = std::rint(x * bits_to_double(0x3ff71547652b82feull));  // x / ln 2
+  const double t = fma_vsv(dn, bits_to_double(0xbfe62e42fefa39efull), x);   // - dn ln2
+  double p = fma_vvs(t, 0x1.9f08a47c8a105p-13, 0x1.6d8cf41dff604p-10);
+  p = fma_vvs(t, p, 0x1.1112708f1c74dp-7);
+  p = fma_vvs(t, p, 0x1.55548dd8721c5p-5);
+  p = fma_vvs(t, p, 0x1.5555544365d72p-3);
+  p = fma_vvs(t, p, 0x1.0000003a1adefp-1);
+  p = fma_vv(t, p, 1.0);
+  p = fma_vv(t, p, 1.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int k = (int)dn;
+#else
+  const int k = (int)std::fmin(std::fmax(dn, -2147483648.0), 2147483647.0);
+#endif
+  double z = std::ldexp(p, k);
+  if (__builtin_expect(!(std::fabs(x) <= 708.0), 0)) {
+    TFG_FM_RARE();
+    z = (x > 1024.0) ? (double)INFINITY : z;
+    z = (x < -1075.0) ? 0.0 : z;
+  }
+  return z;
+}
+
+// exp(c + s) / exp(c) for |s| <= 0.41 (the flux form's lhc / p0 factor,
+// exp(-M g elev / (R T_K)) with its exponent y in [-0.755, 0.065] centred at
+// c = kP0Center, so elevations up to ~5 km at any air temperature): a degree-8
+// polynomial in s with no reduction (scripts/fit_exp.py 8 on [-0.41, 0.41]:
+// 5.1e-12 relative), 8 VALU for exp_p's 12.  The caller folds exp(c) into its
+// constant factor and takes exp_p for a wave with a lane outside the range.
+constexpr double kP0Center = -0.345;
+constexpr double kP0Half = 0.41;
+TFG_FM_HD inline double exp_near(double s) {
+  TFG_FM_NO_CONTRACT
+  double p = fma_vvs(s, 0x1.9deba1dca22f8p-16, 0x1.a215e42a84b4ep-13);
+  p = fma_vvs(s, p, 0x1.6c1acb31a393fp-10);
+  p = fma_vvs(s, p, 0x1.1110390688b5dp-7);
+  p = fma_vvs(s, p, 0x1.5555520449441p-5);
+  p = fma_vvs(s, p, 0x1.555555c3933f1p-3);
+  p = fma_vvs(s, p, 0x1.0000000166a91p-1);
+  p = fma_vv(s, p, 1.0);
+  return fma_vv(s, p, 1.0);
+}
+
+// ---------------------------------------------------------------------------
 // log: fdlibm e_log.c's reduction and polynomial (Lg1..Lg7), one formula for
 // every argument, FMA Horner, s = f / (2 + f) by a Newton reciprocal.
 // ---------------------------------------------------------------------------
@@ -255,6 +307,24 @@ TFG_FM_HD inline double log_k(double x) {
   const double y0 = (double)std::log2((float)x) * 0.69314718055994531;
 #endif
   const double d = fma_vv(x, exp_k(-y0), -1.0);
+  double y = y0 + fma_vv(-0.5 * d, d, d);
+  if (__builtin_expect(!(x >= 0x1p-120 && x < 0x1p120), 0)) {
+    TFG_FM_RARE();
+    y = log_fd(x);
+  }
+  return y;
+}
+
+// log_k's form on exp_p (the fp64-flux form's dew point, round 6): within
+// ~6e-11 absolute (exp_p's error carried into the correction), 4 VALU fewer.
+TFG_FM_HD inline double log_p(double x) {
+  TFG_FM_NO_CONTRACT
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y0 = (double)__builtin_amdgcn_logf((float)x) * 0.69314718055994531;
+#else
+  const double y0 = (double)std::log2((float)x) * 0.69314718055994531;
+#endif
+  const double d = fma_vv(x, exp_p(-y0), -1.0);
   double y = y0 + fma_vv(-0.5 * d, d, d);
   if (__builtin_expect(!(x >= 0x1p-120 && x < 0x1p120), 0)) {
     TFG_FM_RARE();

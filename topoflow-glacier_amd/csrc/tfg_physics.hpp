@@ -95,7 +95,7 @@ struct DevParams {
   double d_eps100, d_ome100;  // 100 eps, 100 (1 - eps): e_air [mbar] = Q P_air / (d_eps100 + d_ome100 Q)   :817-826
   double d_k2;                // (kappa / ln 2)^2: Dn = uz d_k2 / log2((z - h)/z0)^2                       :670-672
   double d_l2k, d_l2kk;       // k, k^2 of the scaled roughness log (f_inv_z0s)
-  double d_qe;                // rho_air Lv lhc 100 / sea_p0                                               :931-934
+  double d_qe;                // rho_air Lv lhc 100 / sea_p0 exp(kP0Center) (the flux form's exp_near)    :931-934
   double d_es_k, d_es_c;      // e_sat(T_s) / e_sat(T_a) = exp(-d_es_k dTs / ((T_s + c)(T_a + c))), c = d_es_c  :788-807
 };
 
@@ -436,6 +436,22 @@ __device__ __forceinline__ double root7(double x) {
   const double y7 = (y2 * y2) * (y2 * y0);
   const double c = (y7 - x) * rcp_nr1(__builtin_fma(4.0, y7, 3.0 * x));  // a correction ~e: 1e-14 of it suffices
   const double y = __builtin_fma(-y0, c, y0);
+  return (x > 0.0 && x < INFINITY) ? y : y0;
+}
+
+// root7 sized for the fp32 engine's fp64-flux form (round 6): the same fp32
+// seed, one Newton step y0 (1 - rho / 7) with rho = (y0^7 - x) / x taken in
+// fp32 (rho ~ 1e-7, so its fp32 rounding is ~1e-14 of y): relative error
+// ~1e-13 (3 rho^2 from Newton), three fp64 operations fewer than root7's Halley
+// step and its fp64 reciprocal.
+__device__ __forceinline__ double root7_p(double x) {
+#pragma clang fp contract(off)
+  const float xf = (float)x;
+  const double y0 = (double)__builtin_amdgcn_exp2f(__builtin_amdgcn_logf(xf) * (1.0f / 7.0f));
+  const double y2 = y0 * y0;
+  const double y7 = (y2 * y2) * (y2 * y0);
+  const float rho7 = (float)(y7 - x) * (__builtin_amdgcn_rcpf(xf) * (1.0f / 7.0f));
+  const double y = __builtin_fma(-y0, (double)rho7, y0);
   return (x > 0.0 && x < INFINITY) ? y : y0;
 }
 
@@ -955,7 +971,10 @@ __device__ __forceinline__ double add_rounded(double h, double a, double b) {
 //   0.00391838 RH^1.5 atan(0.023101 RH), a term below 1e-3 K for RH < 5, with
 //       atan(x) = x (1 - x^2/3 + x^4/5) (relative error x^6/7 < 3e-7 on [0, 5]);
 //   atan(0.151977 sqrt(RH + 8.313659)) as a polynomial fit on [0, 5].
-// Waves with a lane outside [0, 5] (or NaN) take fast_atanf for both.
+// Waves with a lane outside [0, 5] (or NaN) take fast_atanf for both.  The
+// square roots are v_sqrt_f32 alone (within 1 ulp; round 6): the IEEE sqrtf's
+// scaling and two correction steps cost 15 more VALU in every snowing wave for
+// a term below 1e-3 K.
 __device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
   const float a = T_air + rh, b = rh - 1.676331f;
   const float den = fmaf(a, b, 1.0f);
@@ -970,10 +989,10 @@ __device__ __forceinline__ float wet_bulb_f(float rh, float T_air) {
                              -0.003739525331184268f), t, 0.046224694699048996f), t, 0.4634580910205841f);
   if (__any((rh < 0.0f) || (rh > 5.0f))) {  // outside the fits (NaN stays on them)
     const bool off = (rh < 0.0f) || (rh > 5.0f);
-    a0 = off ? fast_atanf(0.151977f * __builtin_sqrtf(rh + 8.313659f)) : a0;
+    a0 = off ? fast_atanf(0.151977f * __builtin_amdgcn_sqrtf(rh + 8.313659f)) : a0;
     at = off ? fast_atanf(x) : at;
   }
-  return T_air * a0 + d + (0.00391838f * (rh * __builtin_sqrtf(rh))) * at - 4.86035f;
+  return T_air * a0 + d + (0.00391838f * (rh * __builtin_amdgcn_sqrtf(rh))) * at - 4.86035f;
 }
 
 // Cold content a snowfall brings (:1507-1537): rho_s Cp_s (P_snow dt ws)
@@ -1115,7 +1134,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
   float e_air, T_dew, T_surf, dTs;
   if constexpr (PREC) {
     e64 = ((double)Hum_sp * (double)P_air) * rcp_nr1(fma((double)Hum_sp, p.d_ome100, p.d_eps100));
-    const double Ld = tfg_fm::log_k(e64 * (1.0 / 6.1121));
+    const double Ld = tfg_fm::log_p(e64 * (1.0 / 6.1121));
     const double Tdew = (257.14 * Ld) * rcp_nr1(18.678 - Ld);
     Tsd = (snow_pos || ice_pos) ? dmin<NS>(Tdew, 0.0) : Tdew;
     dTd = Td - Tsd;
@@ -1153,8 +1172,16 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
     Qh = (p.rho_air_Cp_air * Dhd) * dTd;
     // e_air - e_surf = e_air (1 - e_sat(T_s) / e_sat(T_a)), the exponent difference in one exp
     const double x_es = (-p.d_es_k * dTd) * rcp_nr1((Tsd + p.d_es_c) * (Td + p.d_es_c));
-    const double ded = e64 * (1.0 - tfg_fm::exp_k(x_es));
-    const double p0f = tfg_fm::exp_k(((double)g.ek * 0.69314718055994531) * rcp_nr1(Td + 273.15));  // lhc / p0
+    const double ded = e64 * (1.0 - tfg_fm::exp_p(x_es));
+    // lhc / p0 = exp(y), y = ek ln2 / T_K, as exp(c) exp(y - c) with exp(c) in d_qe
+    const double s0 = fma((double)g.ek * 0.69314718055994531, rcp_nr1(Td + 273.15), -tfg_fm::kP0Center);
+    double p0f;
+    if (__builtin_expect(__any(!(fabs(s0) <= tfg_fm::kP0Half)), 0)) {
+      TFG_FM_RARE();
+      p0f = tfg_fm::exp_p(s0);
+    } else {
+      p0f = tfg_fm::exp_near(s0);
+    }
     Qe = (p.d_qe * Dhd) * ded * p0f;
   } else {
     float bot = (uz * uz) * T_K;
@@ -1259,7 +1286,7 @@ __device__ inline void cell_step_fast(const DevParams& p, const CellStaticF& g, 
     // fp64 engine's; Satterlund's em_air stays fp32), the balance in fp64
     const double TaK = Td + 273.15, TsK = Tsd + 273.15;
     const double emd_m1 = p.satterlund ? (double)em_m1
-                                       : fma(p.one_minus_F_172 * p.cloud_term, root7((e64 * 0.1) * rcp_nr1(TaK)), p.F - 1.0);
+                                       : fma(p.one_minus_F_172 * p.cloud_term, root7_p((e64 * 0.1) * rcp_nr1(TaK)), p.F - 1.0);
     const double ta2d = TaK * TaK;
     Qn_LW = p.em_surf_sigma * fma(emd_m1, ta2d * ta2d, dTd * (TaK + TsK) * fma(TsK, TsK, ta2d));
   } else {
