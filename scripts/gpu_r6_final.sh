@@ -33,10 +33,15 @@ if [ "$PART" = c ]; then
   TAG=$TAG/reh bash scripts/gpu_rehearse.sh
   exit $?
 fi
-PMC_TAG=$TAG/pmc64 PMC_ENGINE=float64 PMC_SHAPE="4096 4096 192" \
+# the fp64-flux form's PMC traffic (round 6: its bench line quotes it)
+PMC_TAG=$TAG/pmcflux PMC_ENGINE=float32_flux64 \
+  PMC_ARGS="--flux fp64 --ny 8192 --nx 8192 --fuse 128 --steps 768 --warmup 128 --no-cpu-baseline --no-dropin --no-parity" \
+  PMC_PROFILE=gpurun_out/$TAG/pmc_8192x8192_fuse128_fluxf64.json bash scripts/gpu_pmc.sh || exit $?
+cp gpurun_out/$TAG/pmc_8192x8192_fuse128_fluxf64.json profiles/pmc_8192x8192_fuse128_fluxf64.json
+[ -n "$SKIP_F64PMC" ] || PMC_TAG=$TAG/pmc64 PMC_ENGINE=float64 PMC_SHAPE="4096 4096 192" \
   PMC_ARGS="--engine float64 --ny 4096 --nx 4096 --fuse 192 --steps 768 --warmup 192 --no-cpu-baseline --no-dropin --no-parity" \
   PMC_PROFILE=gpurun_out/$TAG/pmc_4096x4096_fuse192_f64.json bash scripts/gpu_pmc.sh || exit $?
-cp gpurun_out/$TAG/pmc_4096x4096_fuse192_f64.json profiles/pmc_4096x4096_fuse192_f64.json
+[ -n "$SKIP_F64PMC" ] || cp gpurun_out/$TAG/pmc_4096x4096_fuse192_f64.json profiles/pmc_4096x4096_fuse192_f64.json
 echo "== fp64 bench"
 timeout -k 10 300 python bench.py --engine float64 --ny 4096 --nx 4096 --no-cpu-baseline > gpurun_out/$TAG/bench_f64.log 2>&1
 rc=$?; echo "bench f64 rc=$rc"; grep '^{' gpurun_out/$TAG/bench_f64.log | cut -c1-200

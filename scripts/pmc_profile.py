@@ -80,6 +80,8 @@ KERNELS = {  # engine -> (rocprofv3 kernel-name match, _native symbol prefix, de
     "float32": ("k_fused<float, false, false", "BENCH_KERNEL", "k_fused<float,false,false,false,false,1,false,false> (fp32 engine, clean form"),
     "float64": ("k_fused<double, true, false, false, false", "BENCH_KERNEL_F64",
                 "k_fused<double,true,false,false,false,1,false,false> (fp64 engine"),
+    "float32_flux64": ("k_fused<float, false, false", "BENCH_KERNEL_PREC",
+                       "k_fused<float,false,false,false,false,1,false,true> (fp32 engine, fp64-flux form"),
 }
 
 
@@ -97,7 +99,7 @@ def main():
                       steps=int(sys.argv[7]) if len(sys.argv) > 7 else 8)
     rd4 = scale_of(cal, "read only 4 B/lane", 2.0)
     wr4 = scale_of(cal, "write only 4 B/lane nt", 1.0)
-    if engine == "float32":
+    if engine.startswith("float32"):  # the fp64-flux form moves the fp32 form's bytes
         rd_scale, wr_scale = rd4, wr4
         elem = 4
     else:
