@@ -191,6 +191,9 @@ def parse():
     ap.add_argument("--flux", default="fp32", choices=["fp32", "fp64"],
                     help="the float32 engine's flux arithmetic (tfg_set_flux): fp64 = the dew point, turbulent "
                          "fluxes and long-wave balance in fp64")
+    ap.add_argument("--split", default="auto", choices=["auto", "off", "on"],
+                    help="two-part launches of a small fp32 grid on two streams (tfg_set_split; auto: 2^18 .. 2^24 "
+                         "cells per GPU)")
     ap.add_argument("--scaling", default=None, choices=["weak", "strong"],
                     help="strong (default: one --ny x --nx grid row-partitioned over the ranks, BASELINE "
                          "config 4) or weak (--ny rows per rank)")
@@ -676,6 +679,7 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
         for s in range(steps):
             ev_c[s][0].record(stream)
             eng.run(1)
+            eng.join()  # a split engine's second part (no-op otherwise)
             ev_c[s][1].record(stream)
         torch.cuda.synchronize(eng.device)
         c_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_c]))
@@ -696,11 +700,13 @@ def dropin_grid_leg(eng, args, torch, stream, steps: int = 24) -> dict:
                 eng.set_inputs(blk, index=eng.step_index % args.frames)
                 ev_k[s][0].record(stream)
                 eng.run(1)
+                eng.join()  # a split engine's second part (no-op otherwise)
                 ev_k[s][1].record(stream)
         else:
             for s in range(steps):
                 eng.set_inputs(blk, index=(eng.step_index + s) % args.frames)
             eng.run(steps)
+        eng.join()
         e1.record(stream)
         torch.cuda.synchronize(eng.device)
         wall = time.perf_counter() - t0
@@ -884,7 +890,7 @@ def main(args=None):
             depth_note = f"{auto}-step history over the {DEVICE_BYTES_BUDGET / 1e9:.0f} GB budget; fused {args.fuse} steps"
     def create(depth: int):
         return GlacierEngine(cfg, rows, args.nx, engine=args.engine, device=local, n_frames=args.frames, flux=args.flux,
-                             hist_depth=depth, fuse_steps=depth, row0=row0, n_catch=n_catch)
+                             hist_depth=depth, fuse_steps=depth, row0=row0, n_catch=n_catch, split=args.split)
 
     eng, create_error = None, None
     while True:
@@ -963,18 +969,31 @@ def main(args=None):
     steps = timed_steps(args.steps, args.fuse, fuse_explicit)
     n_launch = steps // args.fuse
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_launch)]
+    # A split engine (tfg_set_split: a grid of <= 2^24 cells as two parts on two
+    # streams) overlaps one part's launch with the other's: per-launch events on
+    # the engine's stream would bracket the first parts only, so its launch time
+    # is the span of the timed region (both parts joined) over the launches.
+    split = eng.is_split()
     barrier()
     t0 = time.perf_counter()
     for i in range(n_launch):
         if args.conduction:
             conduct()
-        ev[i][0].record(stream)
+        if not split or i == 0:
+            ev[i][0].record(stream)
         eng.run(args.fuse)
-        ev[i][1].record(stream)
+        if not split:
+            ev[i][1].record(stream)
+    if split:
+        eng.join()
+        ev[-1][1].record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
     note(f"timed region: {n_launch} launches of {args.fuse} steps in {elapsed:.3f} s")
-    launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    if split:
+        launch_ms = np.full(n_launch, ev[0][0].elapsed_time(ev[-1][1]) / n_launch)
+    else:
+        launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
     cells = rows * args.nx
     diag = allreduce_diagnostics(eng.diagnostics()) if pg else eng.diagnostics()
     bytes_launch = cells * launch_bytes_per_cell(args.fuse, elem, args.catchments > 0, args.conduction)
@@ -1062,6 +1081,7 @@ def main(args=None):
                 "grid_per_gpu": [rows, args.nx],
                 "frames": args.frames,
                 "fuse_steps": args.fuse,
+                "launch_parts": 2 if split else 1,
                 "parallelism": f"row-block x{world}",
             },
             "roofline": {
@@ -1074,6 +1094,10 @@ def main(args=None):
                 "traffic_source": traffic_source,
                 "bytes_per_cell_update": bytes_launch / (cells * args.fuse),
                 "kernel_ms_per_launch": float(launch_ms.mean()),
+                "launch_time_source": ("HIP events on the engine's stream: the span of the timed region (the second "
+                                       "part joined) / launches; split launches, two parts on two streams "
+                                       "(tfg_set_split), overlap" if split else
+                                       "HIP events on the engine's stream around every launch"),
                 "bytes_model": dict(zip(("per_step", "per_launch"), bytes_model(elem, args.catchments > 0, args.conduction))),
                 "note": None if args.engine == "float32" else (
                     "the fp64 engine is issue-bound, not HBM-bound: its step issues ~680 VALU instructions per "

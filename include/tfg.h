@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define TFG_ABI_VERSION 7
+#define TFG_ABI_VERSION 8
 
 /* status codes */
 enum {
@@ -302,6 +302,32 @@ int tfg_set_step_form(tfg_handle* h, int form);
 #define TFG_FLUX_F32 0
 #define TFG_FLUX_F64 1
 int tfg_set_flux(tfg_handle* h, int flux);
+
+/* Split launches (ABI 8, round 6).  A grid of at most 2^24 cells fills the
+ * chip's resident workgroups only a few times per launch, and the end of every
+ * launch drains with most slots idle.  The fp32 engine then steps it as two
+ * parts of about half the cells each, the second on a second stream of its own
+ * with its own copy of the step uniforms: one part's next launch fills the other
+ * part's drain (+4-5 % at 1024^2 and 4096^2; none at 8192^2, which runs one part).
+ * Results are the same bit for bit (the update is pointwise; each part's
+ * workgroups fold their diagnostics into the slab rows of their own cells).
+ *   TFG_SPLIT_AUTO  (default) split fp32-engine grids of 2^18 (one round of the
+ *                   resident workgroups) to 2^24 cells
+ *   TFG_SPLIT_OFF   one launch over the whole grid
+ *   TFG_SPLIT_ON    split every fp32-engine grid of at least 512 cells (tests)
+ * While split, tfg_step returns with the second part's launches queued on the
+ * second stream only: every other call of this API orders the handle's stream
+ * after them first, and tfg_join does just that (without waiting on the host),
+ * for a caller that queues its own work on the handle's stream (tfg_get_stream)
+ * after tfg_step, e.g. an event marking the steps' end.  No reference
+ * counterpart (the reference is single-threaded NumPy). */
+#define TFG_SPLIT_AUTO 0
+#define TFG_SPLIT_OFF 1
+#define TFG_SPLIT_ON 2
+int tfg_set_split(tfg_handle* h, int mode);
+int tfg_join(tfg_handle* h);
+/* 1 if the handle's next tfg_step runs split, else 0. */
+int tfg_get_split(tfg_handle* h, int* split);
 
 /* Self-test of the fp64 engine's power rewrites on the device (tests only):
  * out[i] = pow4(x[i]) (which = 0: T^4, :1231-1233), pow1p5(x[i]) (1: RH^1.5,

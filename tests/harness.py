@@ -355,13 +355,13 @@ def split_engine(engine: str) -> tuple[str, str]:
 
 
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
-                fuse_steps: int = 24, row0: int = 0, flux: str = "fp32"):
+                fuse_steps: int = 24, row0: int = 0, flux: str = "fp32", split: str = "auto"):
     from topoflow_glacier.engine import GlacierEngine
 
     engine, f = split_engine(engine)
     return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
                          hist_depth=hist_depth, n_catch=n_catch, fuse_steps=fuse_steps, row0=row0,
-                         flux=f if f == "fp64" else flux)
+                         flux=f if f == "fp64" else flux, split=split)
 
 
 def gpu_run_fields(cfg: dict, static: dict, forcing: dict, ny: int, nx: int, engine: str, nsteps: int,

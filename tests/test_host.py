@@ -186,7 +186,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 17
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing
-    assert L.tfg_abi_version() == _native.ABI_VERSION == 7
+    assert L.tfg_abi_version() == _native.ABI_VERSION == 8
     assert b"gfx950" in L.tfg_build_info()
 
 

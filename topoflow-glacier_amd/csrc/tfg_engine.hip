@@ -670,6 +670,16 @@ struct tfg_handle {
   int64_t ns_launches = 0;           // launches that ran the NaN-safe form (tfg_nan_safe_launches)
   bool force_ns = false;             // tfg_set_step_form(TFG_FORM_NAN_SAFE): every launch NaN-safe
   bool flux_f64 = false;             // tfg_set_flux(TFG_FLUX_F64): the fp32 engine's fp64-flux form
+  // Split launches (tfg_set_split): the second part's stream, its copy of the
+  // step uniforms, and the events that order it against the handle's stream
+  int split_mode = TFG_SPLIT_AUTO;
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
+  tfg_uniforms* d_u2 = nullptr;
+  int64_t d_u2_cap = 0;
+  hipEvent_t h_u_ev2[2] = {nullptr, nullptr};
+  bool side_busy = false;   // the side stream holds launches the handle's stream is not yet ordered after
+  bool side_stale = true;   // the handle's stream holds work the side stream's next launch must follow
   std::string err;
 };
 
@@ -694,6 +704,48 @@ int ensure_qc(tfg_handle* h) {
   if (h->qc) return TFG_OK;
   HIPCHK(h, hipMalloc(&h->qc, (size_t)h->n_pad * h->rsz));
   HIPCHK(h, hipMemsetAsync(h->qc, 0, (size_t)h->n_pad * h->rsz, h->stream));
+  return TFG_OK;
+}
+
+// Split launches (include/tfg.h tfg_set_split).  The parts are whole 256-cell
+// chunks; AUTO splits grids of one to 64 rounds of the resident workgroups.
+bool split_active(const tfg_handle* h) {
+  if (h->engine != TFG_F32 || h->split_mode == TFG_SPLIT_OFF) return false;
+  if (h->split_mode == TFG_SPLIT_ON) return h->n_pad >= 2 * kBlock;
+  return h->n >= ((int64_t)1 << 18) && h->n <= ((int64_t)1 << 24);
+}
+// The handle's stream after the side stream's launches so far (no host wait).
+int join_side(tfg_handle* h) {
+  if (!h->side_busy) return TFG_OK;
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipEventRecord(h->side_join, h->side));
+  HIPCHK(h, hipStreamWaitEvent(h->stream, h->side_join, 0));
+  h->side_busy = false;
+  return TFG_OK;
+}
+// The side stream after the handle's stream's work so far: only when that
+// holds something other than the first parts' launches (a field set, the
+// window totals, ...), so consecutive tfg_step calls leave the streams free.
+int fork_side(tfg_handle* h) {
+  if (!h->side_stale) return TFG_OK;
+  HIPCHK(h, hipEventRecord(h->side_fork, h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->side, h->side_fork, 0));
+  h->side_stale = false;
+  return TFG_OK;
+}
+// Every API call but tfg_step: order the handle's stream after the side's
+// launches, and have the side's next launch follow what the call queues.
+int api_sync(tfg_handle* h) {
+  if (!h) return TFG_OK;
+  h->side_stale = true;
+  return join_side(h);
+}
+int ensure_side(tfg_handle* h) {
+  if (h->side) return TFG_OK;
+  HIPCHK(h, hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+  HIPCHK(h, hipEventCreateWithFlags(&h->side_fork, hipEventDisableTiming));
+  HIPCHK(h, hipEventCreateWithFlags(&h->side_join, hipEventDisableTiming));
+  h->side_stale = true;
   return TFG_OK;
 }
 
@@ -933,9 +985,18 @@ struct IoArgs {
   uint8_t in_state = kUnknown;  // the inputs' finite-data status (tfg_handle::plane_state)
 };
 
+// One part of a split launch (launch_steps): cells [c0, c0 + cells) of the
+// plane stride, n_valid of them grid cells, on `stream` with its own uniforms;
+// its workgroups fold into slab rows from slab_row0.
+struct Part {
+  int64_t c0, cells, n_valid, slab_row0;
+  hipStream_t stream;
+};
+
 template <class R, bool EXACT>
-int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns) {
-  const hipStream_t stream = h->stream;
+int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size_t lds, const IoArgs& io, bool ns,
+                 const Part* part = nullptr) {
+  const hipStream_t stream = part ? part->stream : h->stream;
   KArgs a;
   a.p = h->dp;
   a.K = K;
@@ -944,25 +1005,31 @@ int launch_fused(tfg_handle* h, const tfg_uniforms* d_u, int K, int blocks, size
   a.io_flag = io.flag;
   a.io_seq = io.seq;
   a.n_catch = h->n_catch;
-  a.n = h->n;
+  a.n = part ? part->n_valid : h->n;
   a.n_pad = h->n_pad;
+  a.n_step = part ? part->cells : h->n_pad;
+  // a part's buffers start at its first cell in every plane (the planes keep
+  // their stride); the kernel corrects its two mixed-width views by c0
+  const int64_t c0 = part ? part->c0 : 0;
+  a.part_c0 = c0;
+  const size_t rb = (size_t)c0 * h->rsz;
+  const FusedBufs fb = {d_u, static_cast<const char*>(h->forc) + rb, static_cast<const char*>(h->stat) + rb, h->geo + c0,
+                        h->catch_id ? h->catch_id + c0 : nullptr, h->st + c0, h->tot + c0, h->ring + c0,
+                        static_cast<char*>(h->hist) + rb, h->slab + (part ? part->slab_row0 : 0) * h->n_catch * 6,
+                        h->qc ? static_cast<const char*>(h->qc) + rb : nullptr};
   const bool rd = !h->depths_derived;
   const bool ct = h->catch_id != nullptr;
   if constexpr (EXACT) {  // the fp64 engine's instantiations live in tfg_fused_f64.hip
-    const FusedBufs fb = {d_u, h->forc, h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->slab,
-                          h->qc};
     HIPCHK(h, launch_fused_exact(a, fb, rd, ct, h->qc_on, blocks, lds, stream));
     return TFG_OK;
   } else {
   if (h->flux_f64) {  // the fp64-flux form's instantiations live in tfg_fused_prec.hip
-    const FusedBufs fb = {d_u, h->forc, h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->slab,
-                          h->qc};
     HIPCHK(h, launch_fused_prec(a, fb, rd, ct, h->qc_on, ns, blocks, lds, stream));
     return TFG_OK;
   }
   constexpr int C = kCellsPerThread;
-#define TFG_ARGS a, d_u, (const R*)h->forc, (const R*)h->stat, h->geo, h->catch_id, h->st, h->tot, h->ring, (R*)h->hist, \
-                 h->slab, (const R*)h->qc
+#define TFG_ARGS a, d_u, (const R*)fb.forc, (const R*)fb.stat, fb.geo, fb.catch_id, fb.st, fb.tot, fb.ring, (R*)fb.hist, \
+                 fb.slab, (const R*)fb.qc
 #define TFG_LAUNCH(RD, CT, QC, NS) \
   hipLaunchKernelGGL((k_fused<R, EXACT, RD, CT, QC, C, NS>), blocks, kBlock, lds, stream, TFG_ARGS)
 #define TFG_LAUNCH_NS(RD, CT, QC) \
@@ -1136,13 +1203,15 @@ int tfg_destroy(tfg_handle* h) {
   // work queued on a caller's stream (tfg_set_stream) may still use the buffers
   if (h->stream && h->stream != h->own_stream) (void)hipStreamSynchronize(h->stream);
   if (h->own_stream) (void)hipStreamSynchronize(h->own_stream);
+  if (h->side) (void)hipStreamSynchronize(h->side);
   void* ptrs[] = {h->forc, h->stat, h->lwsw, h->geo, h->catch_id, h->st, h->tot, h->ring, h->hist, h->diag, h->wtmp, h->halo,
                   h->flow_halo, h->flow_edges, h->flow_red, h->qc, h->cond_halo, h->cond_edges,
-                  h->slab, h->d_diurnal, h->d_flag, h->d_u, h->staging};
+                  h->slab, h->d_diurnal, h->d_flag, h->d_u, h->d_u2, h->staging};
   for (void* q : ptrs) if (q) (void)hipFree(q);
   for (int i = 0; i < 2; ++i) {
     if (h->h_u[i]) (void)hipHostFree(h->h_u[i]);
     if (h->h_u_ev[i]) (void)hipEventDestroy(h->h_u_ev[i]);
+    if (h->h_u_ev2[i]) (void)hipEventDestroy(h->h_u_ev2[i]);
     if (h->in_h[i]) (void)hipHostFree(h->in_h[i]);
     if (h->in_d[i]) (void)hipFree(h->in_d[i]);
     if (h->in_ev[i]) (void)hipEventDestroy(h->in_ev[i]);
@@ -1151,11 +1220,15 @@ int tfg_destroy(tfg_handle* h) {
   if (h->out_h) (void)hipHostFree(h->out_h);
   if (h->io_h) (void)hipHostFree(h->io_h);
   if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+  if (h->side_fork) (void)hipEventDestroy(h->side_fork);
+  if (h->side_join) (void)hipEventDestroy(h->side_join);
+  if (h->side) (void)hipStreamDestroy(h->side);
   delete h;
   return TFG_OK;
 }
 
 int tfg_set_stream(tfg_handle* h, void* stream) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   h->stream = stream ? static_cast<hipStream_t>(stream) : h->own_stream;
   return TFG_OK;
@@ -1187,6 +1260,7 @@ int tfg_shared_stream(int device, void** stream) {
 }
 
 int tfg_get_stream(tfg_handle* h, void** stream) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !stream) return fail(h, TFG_ERR_ARG, "null argument");
   *stream = h->stream;
   return TFG_OK;
@@ -1210,8 +1284,28 @@ int tfg_set_flux(tfg_handle* h, int flux) {
   return TFG_OK;
 }
 
+int tfg_set_split(tfg_handle* h, int mode) {
+  if (!h || (mode != TFG_SPLIT_AUTO && mode != TFG_SPLIT_OFF && mode != TFG_SPLIT_ON))
+    return fail(h, TFG_ERR_ARG, "split must be TFG_SPLIT_AUTO, TFG_SPLIT_OFF or TFG_SPLIT_ON");
+  if (int rc = api_sync(h)) return rc;
+  h->split_mode = mode;
+  return TFG_OK;
+}
+
+int tfg_join(tfg_handle* h) {
+  if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
+  return join_side(h);
+}
+
+int tfg_get_split(tfg_handle* h, int* split) {
+  if (!h || !split) return fail(h, TFG_ERR_ARG, "null argument");
+  *split = split_active(h) ? 1 : 0;
+  return TFG_OK;
+}
+
 int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_dtype, int64_t n,
                   int src_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!src) return fail(h, TFG_ERR_ARG, "null src");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n = " + std::to_string(n) + " != ny*nx = " + std::to_string(h->n));
@@ -1334,6 +1428,7 @@ int tfg_set_field(tfg_handle* h, int field, int index, const void* src, int src_
 }
 
 int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
   if (n <= 0 || n > h->n) return fail(h, TFG_ERR_ARG, "n outside 1..ny*nx");  // n < ny*nx: the first n cells
@@ -1382,6 +1477,7 @@ int tfg_get_field(tfg_handle* h, int field, int index, void* dst, int dst_dtype,
 }
 
 int tfg_init_state(tfg_handle* h) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
   const DevParams& p = h->dp;
@@ -1417,14 +1513,16 @@ int check_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
 
 // The launches of nsteps steps whose uniforms the device reads at d_u (u is
 // the host copy of the same records).
-int fused_blocks(const tfg_handle* h) {
-  const int64_t ngroups = h->n_pad / kCellsPerThread;  // k_fused steps the whole plane stride
-  return (int)std::min<int64_t>(std::max<int64_t>((ngroups + kBlock - 1) / kBlock, 1), h->max_blocks);
+int64_t chunks_of(int64_t cells) { return (cells / kCellsPerThread + kBlock - 1) / kBlock; }
+int fused_blocks(const tfg_handle* h) {  // k_fused steps the whole plane stride
+  return (int)std::min<int64_t>(std::max<int64_t>(chunks_of(h->n_pad), 1), h->max_blocks);
 }
 
 // Work a launch of the step kernels depends on: window totals after slots were
 // set, and the per-cell geometry after the static rasters changed.
 int prepare_steps(tfg_handle* h) {
+  if (h->tot_dirty || h->geo_dirty)  // rewrites planes a split launch's second part may still read
+    if (int rc = api_sync(h)) return rc;
   if (h->tot_dirty) {  // window slots were set: rebuild the running totals
     hipLaunchKernelGGL(k_window_total, grid_for(h->n_pad), 256, 0, h->stream, h->tot, h->ring, h->ring_len, h->n_pad);
     HIPCHK(h, hipGetLastError());
@@ -1531,6 +1629,7 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
     }
   }
   if (check && (h->state_state == kUnknown || (h->state_state == kDirty && --h->state_recheck <= 0))) {
+    if (int rc = api_sync(h)) return rc;  // the state a split launch's second part writes
     if (int rc = check_state(h)) return rc;
     if (h->state_state == kDirty) h->state_recheck = kVerifySteps;  // launches until the next look
   }
@@ -1544,7 +1643,7 @@ int choose_form(tfg_handle* h, const tfg_uniforms* u, int K, const IoArgs& io, b
 }
 
 int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, int64_t nsteps,
-                 const IoArgs& io = IoArgs()) {
+                 const IoArgs& io = IoArgs(), bool split = false) {
   if (int rc = prepare_steps(h)) return rc;
   const int blocks = fused_blocks(h);
   const size_t lds = (size_t)kWaves * h->n_catch * 6 * sizeof(double);
@@ -1563,6 +1662,8 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
       a.n_catch = h->n_catch;
       a.n = h->n;
       a.n_pad = h->n_pad;
+      a.n_step = h->n_pad;
+  a.n_step = h->n_pad;
       a.io_in = nullptr;
       a.io_out = nullptr;
       a.io_flag = nullptr;
@@ -1572,6 +1673,28 @@ int launch_steps(tfg_handle* h, const tfg_uniforms* d_u, const tfg_uniforms* u, 
                          static_cast<double*>(h->hist), h->slab, h->qc_on ? static_cast<const double*>(h->qc) : nullptr,
                          h->depths_derived ? 0 : 1);
       HIPCHK(h, hipGetLastError());
+    } else if (h->engine == TFG_F32 && split && !io.in) {
+      // two parts on two streams: the first on the handle's stream, the second
+      // on the side stream with its own uniforms (tfg_step copied them there)
+      bool ns = true;
+      if ((rc = choose_form(h, u + k0, K, io, &ns))) return rc;
+      if ((rc = fork_side(h))) return rc;
+      // an odd chunk count for the first part: the parts' planes then do not sit a
+      // power of two apart (+0.3-0.5 % at 2048^2 against an even split, same box)
+      const int64_t chA = (chunks_of(h->n_pad) / 2) | 1, chB = chunks_of(h->n_pad) - chA;
+      const int64_t nA = chA * kBlock * kCellsPerThread;
+      const bool fit = chA + chB <= h->max_blocks;  // one workgroup per chunk, as unsplit
+      const int bA = (int)(fit ? chA : std::min<int64_t>(chA, h->max_blocks / 2));
+      const int bB = (int)(fit ? chB : std::min<int64_t>(chB, h->max_blocks / 2));
+      const Part pa = {0, nA, std::min(h->n, nA), 0, h->stream};
+      const Part pb = {nA, h->n_pad - nA, std::max<int64_t>(h->n - nA, 0), bA, h->side};
+      if ((rc = launch_fused<float, false>(h, d_u + k0, K, bA, lds, io, ns, &pa))) return rc;
+      if ((rc = launch_fused<float, false>(h, h->d_u2 + k0, K, bB, lds, io, ns, &pb))) return rc;
+      h->side_busy = true;
+      if (ns) {
+        ++h->ns_launches;
+        if (h->state_state == kOk) h->state_state = kUnknown;
+      }
     } else if (h->engine == TFG_F32) {
       bool ns = true;
       if ((rc = choose_form(h, u + k0, K, io, &ns))) return rc;
@@ -1598,11 +1721,18 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   if (nsteps <= 0) return TFG_OK;
   if (int rc = check_step(h, u, nsteps)) return rc;
   HIPCHK(h, hipSetDevice(h->device));
-  // stage uniforms: pinned double buffer -> device array
+  const bool split = split_active(h);
+  if (split) {
+    if (int rc = ensure_side(h)) return rc;
+  } else if (int rc = api_sync(h)) {  // a handle that stopped splitting (tfg_set_split)
+    return rc;
+  }
+  // stage uniforms: pinned double buffer -> device array (and the side stream's copy)
   const int b = h->h_u_next;
   h->h_u_next ^= 1;
   if (h->h_u_ev[b]) HIPCHK(h, hipEventSynchronize(h->h_u_ev[b]));
   else HIPCHK(h, hipEventCreateWithFlags(&h->h_u_ev[b], hipEventDisableTiming));
+  if (h->h_u_ev2[b]) HIPCHK(h, hipEventSynchronize(h->h_u_ev2[b]));
   if (h->h_u_cap[b] < nsteps) {
     if (h->h_u[b]) HIPCHK(h, hipHostFree(h->h_u[b]));
     h->h_u[b] = nullptr;
@@ -1620,10 +1750,23 @@ int tfg_step(tfg_handle* h, const tfg_uniforms* u, int64_t nsteps) {
   std::memcpy(h->h_u[b], u, (size_t)nsteps * sizeof(tfg_uniforms));
   HIPCHK(h, hipMemcpyAsync(h->d_u, h->h_u[b], (size_t)nsteps * sizeof(tfg_uniforms), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipEventRecord(h->h_u_ev[b], h->stream));
-  return launch_steps(h, h->d_u, u, nsteps);
+  if (split) {
+    if (h->d_u2_cap < nsteps) {
+      HIPCHK(h, hipStreamSynchronize(h->side));  // its launches may still read d_u2
+      if (h->d_u2) HIPCHK(h, hipFree(h->d_u2));
+      h->d_u2 = nullptr;
+      HIPCHK(h, hipMalloc((void**)&h->d_u2, (size_t)nsteps * sizeof(tfg_uniforms)));
+      h->d_u2_cap = nsteps;
+    }
+    if (!h->h_u_ev2[b]) HIPCHK(h, hipEventCreateWithFlags(&h->h_u_ev2[b], hipEventDisableTiming));
+    HIPCHK(h, hipMemcpyAsync(h->d_u2, h->h_u[b], (size_t)nsteps * sizeof(tfg_uniforms), hipMemcpyHostToDevice, h->side));
+    HIPCHK(h, hipEventRecord(h->h_u_ev2[b], h->side));
+  }
+  return launch_steps(h, h->d_u, u, nsteps, IoArgs(), split);
 }
 
 int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !out) return fail(h, TFG_ERR_ARG, "null argument");
   if (n_catch != h->n_catch) return fail(h, TFG_ERR_ARG, "n_catch mismatch");
   HIPCHK(h, hipSetDevice(h->device));
@@ -1638,6 +1781,7 @@ int tfg_get_diag(tfg_handle* h, double* out, int n_catch) {
 }
 
 int tfg_reset_diag(tfg_handle* h) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipMemsetAsync(h->slab, 0, (size_t)h->max_blocks * h->n_catch * 6 * 8, h->stream));
@@ -1679,6 +1823,7 @@ int tfg_nan_safe_launches(tfg_handle* h, int64_t* count) {
 }
 
 int tfg_sync(tfg_handle* h) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1687,6 +1832,7 @@ int tfg_sync(tfg_handle* h) {
 
 int tfg_fill_synthetic(tfg_handle* h, uint64_t seed, int64_t row0, int64_t nx_global, const float* diurnal,
                        int n_frames) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !diurnal) return fail(h, TFG_ERR_ARG, "null argument");
   if (n_frames != h->n_frames) return fail(h, TFG_ERR_ARG, "n_frames mismatch");
   if (nx_global != h->nx) return fail(h, TFG_ERR_ARG, "row-block shards must span full rows (nx_global == nx)");
@@ -1717,6 +1863,7 @@ int launch_gather(tfg_handle* h, int hist, void* gdst, int dst_dtype, int64_t n)
 }  // namespace
 
 int tfg_set_inputs(tfg_handle* h, int frame, const void* src, int src_dtype, int64_t n, int src_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!src) return fail(h, TFG_ERR_ARG, "null src");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
@@ -1799,6 +1946,7 @@ int launch_gather(tfg_handle* h, int hist, void* gdst, int dst_dtype, int64_t n)
 }  // namespace
 
 int tfg_get_outputs(tfg_handle* h, int hist, void* dst, int dst_dtype, int64_t n, int dst_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!dst) return fail(h, TFG_ERR_ARG, "null dst");
   if (n != h->n) return fail(h, TFG_ERR_ARG, "n != ny*nx");
@@ -1864,6 +2012,7 @@ int wait_flags(tfg_handle* h, size_t flag_off, int blocks, uint32_t seq) {
 
 int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const tfg_uniforms* u, void* dst,
                int dst_dtype, int64_t n) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   TFG_TSTAMP(t_in0);
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!src || !dst) return fail(h, TFG_ERR_ARG, "null src/dst");
@@ -1910,6 +2059,7 @@ int tfg_update(tfg_handle* h, int frame, const void* src, int src_dtype, const t
     a.n_catch = h->n_catch;
     a.n = h->n;
     a.n_pad = h->n_pad;
+    a.n_step = h->n_pad;
     a.io_in = nullptr;
     a.io_out = reinterpret_cast<double*>(h->io_d + out_off);
     a.io_flag = reinterpret_cast<uint32_t*>(h->io_d + flag_off);
@@ -1999,6 +2149,8 @@ ManyBlock g_many[kMaxDevices];
 
 int tfg_update_many(tfg_handle* const* hs, int m, const double* const* src, const tfg_uniforms* const* u,
                     double* const* dst) {
+  for (int i = 0; hs && i < m; ++i)
+    if (int rc_ = api_sync(hs[i])) return rc_;  // after a split launch's second part
   if (m <= 0) return TFG_OK;
   if (!hs || !src || !u || !dst) return fail(nullptr, TFG_ERR_ARG, "tfg_update_many: null argument");
   tfg_handle* h0 = hs[0];
@@ -2084,6 +2236,7 @@ int tfg_update_many(tfg_handle* const* hs, int m, const double* const* src, cons
 
 int tfg_terrain_from_dem(tfg_handle* h, double dx, double dy, const void* halo_north, const void* halo_south,
                          int halo_dtype, int halo_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
   if (halo_dtype != TFG_F32 && halo_dtype != TFG_F64) return fail(h, TFG_ERR_ARG, "halo dtype must be TFG_F32/TFG_F64");
@@ -2139,6 +2292,7 @@ int flow_setup(tfg_handle* h, const double* hn, const double* hs, int on_dev, Fl
 }  // namespace
 
 int tfg_ice_flow_edges(tfg_handle* h, double* first, double* last, int on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !first || !last) return fail(h, TFG_ERR_ARG, "null argument");
   HIPCHK(h, hipSetDevice(h->device));
   FlowGrid g;
@@ -2160,6 +2314,7 @@ int tfg_ice_flow_edges(tfg_handle* h, double* first, double* last, int on_device
 
 int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_north, const double* halo_south,
                       int halo_on_device, double* dmax) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !dmax) return fail(h, TFG_ERR_ARG, "null argument");
   if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
   HIPCHK(h, hipSetDevice(h->device));
@@ -2187,6 +2342,7 @@ int tfg_ice_flow_dmax(tfg_handle* h, double dx, double dy, const double* halo_no
 
 int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, const double* halo_north,
                       const double* halo_south, int halo_on_device, int part) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0) || !(dt_years > 0)) return fail(h, TFG_ERR_ARG, "dt, dx and dy must be > 0");
   if (part != TFG_FLOW_ALL && part != TFG_FLOW_INTERIOR && part != TFG_FLOW_EDGES)
@@ -2224,6 +2380,7 @@ int tfg_ice_flow_step(tfg_handle* h, double dt_years, double dx, double dy, cons
 }
 
 int tfg_ice_flow_run(tfg_handle* h, double dt_years, double dx, double dy, int n_sub) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0) || !(dt_years > 0) || n_sub < 1) return fail(h, TFG_ERR_ARG, "dt, dx, dy and n_sub must be > 0");
   HIPCHK(h, hipSetDevice(h->device));
@@ -2285,6 +2442,7 @@ int cond_setup(tfg_handle* h, const double* hn, const double* hs, int on_dev, tf
 }  // namespace
 
 int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h || !first || !last) return fail(h, TFG_ERR_ARG, "null argument");
   HIPCHK(h, hipSetDevice(h->device));
   tfg::CondGrid g;
@@ -2302,6 +2460,7 @@ int tfg_conduction_edges(tfg_handle* h, double* first, double* last, int on_devi
 
 int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx, double dy, double q_ground,
                           const double* halo_north, const double* halo_south, int halo_on_device) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   if (!(dx > 0) || !(dy > 0)) return fail(h, TFG_ERR_ARG, "dx and dy must be > 0");
   if (!(k_snow >= 0) || !(k_ice >= 0)) return fail(h, TFG_ERR_ARG, "conductivities must be >= 0");
@@ -2332,6 +2491,7 @@ int tfg_conduction_update(tfg_handle* h, double k_snow, double k_ice, double dx,
 }
 
 int tfg_conduction_off(tfg_handle* h) {
+  if (int rc_ = api_sync(h)) return rc_;  // after a split launch's second part
   if (!h) return fail(nullptr, TFG_ERR_ARG, "null handle");
   h->qc_on = false;
   if (h->qc) {

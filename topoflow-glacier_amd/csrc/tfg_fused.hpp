@@ -52,6 +52,14 @@ struct KArgs {
   double* io_out;
   uint32_t* io_flag;  // [gridDim] in the same block: io_seq once a workgroup is done
   uint32_t io_seq;
+  // The cells a k_fused launch steps: n_pad, or one part of a split launch
+  // (tfg_engine.hip launch_steps: a small grid as two parts on two streams,
+  // the second part's buffers offset by its first cell, part_c0).  Two planes
+  // are read through a pointer of another width than their buffer's (the fp64
+  // geometry planes after the fp32 ones, the fp32 albedo in an fp64 state
+  // plane): the kernel corrects those by part_c0.
+  int64_t n_step = 0;
+  int64_t part_c0 = 0;
 };
 
 // TFG_STEP_PARAMS(p): inside a step loop, `p` names the launch's model
@@ -197,8 +205,9 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
 
   const int64_t n_pad = a.n_pad;
   // the whole plane stride, the skew's padding cells included (stepping only the cells
-  // measured neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, profiles/r4d_ab_skew.json)
-  const int64_t ngroups = n_pad / C;
+  // measured neutral: -0.5 % at 8192^2, +0.6 % at 1024^2, profiles/r4d_ab_skew.json),
+  // or one part of a split launch
+  const int64_t ngroups = a.n_step / C;
   // Workgroups own whole, aligned chunks of kBlock cell groups, for any grid
   // size: every trip is one full, 64-cell-aligned wave per lane group (a
   // partition in single cells leaves misaligned ranges and a ragged last trip).
@@ -207,7 +216,10 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
   const int64_t g0 = (wg * nchunks / gridDim.x) * kBlock;
   const int64_t g1 = std::min<int64_t>(((wg + 1) * nchunks / gridDim.x) * kBlock, ngroups);
   const int64_t trips = (g1 - g0 + kBlock - 1) / kBlock;
-  const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad);
+  // the pointer arithmetic of a part's float geo moved these by part_c0 / 2 doubles, not part_c0
+  const double* geo_d = reinterpret_cast<const double*>(geo + tfg::kGeoF * n_pad) + a.part_c0 / 2;
+  // and a part's double st moved the fp32 albedo plane by 2 part_c0 floats, not part_c0
+  float* const alb_f = reinterpret_cast<float*>(st + S_ALB * n_pad) - a.part_c0;
 
   CellDiag acc;
   diag_zero(acc);
@@ -300,7 +312,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
           }
           if (__any(carried)) {
             float fa[C];
-            vload<float, C>(reinterpret_cast<const float*>(st + S_ALB * n_pad), lc, fa);
+            vload<float, C>(alb_f, lc, fa);
 #pragma unroll
             for (int j = 0; j < C; ++j) cs[j].albedo = (double)fa[j];
           }
@@ -488,7 +500,7 @@ __global__ __launch_bounds__(kBlock, EXACT ? kMinWavesExact : (PREC ? kMinWavesP
           float fa[C];
 #pragma unroll
           for (int j = 0; j < C; ++j) fa[j] = (float)cs[j].albedo;
-          vstore<float, C>(reinterpret_cast<float*>(st + S_ALB * n_pad), lc, fa);
+          vstore<float, C>(alb_f, lc, fa);
         }
         int64_t t[C];
 #pragma unroll

@@ -20,7 +20,7 @@ __all__ = [
 
 LIB_PATH = Path(os.environ.get("TFG_LIB", Path(__file__).resolve().parent / "_tfg.so"))
 
-ABI_VERSION = 7  # include/tfg.h TFG_ABI_VERSION
+ABI_VERSION = 8  # include/tfg.h TFG_ABI_VERSION
 FLOW_ALL, FLOW_INTERIOR, FLOW_EDGES = 0, 1, 2  # tfg_ice_flow_step parts
 PREV_DEPTH = -1  # tfg_get_field / tfg_set_field index: the fp64 previous-step depth (TFG_PREV_DEPTH)
 F32, F64, I32 = 0, 1, 2
@@ -126,6 +126,9 @@ def load() -> ctypes.CDLL:
         "tfg_nan_safe_launches": ([vp, ctypes.POINTER(i64)], i32),
         "tfg_set_step_form": ([vp, i32], i32),
         "tfg_set_flux": ([vp, i32], i32),
+        "tfg_set_split": ([vp, i32], i32),
+        "tfg_join": ([vp], i32),
+        "tfg_get_split": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
         "tfg_selftest_powers": ([i32, vp, i64, i32, vp], i32),
     }
     for name, (args, res) in sigs.items():
@@ -134,7 +137,9 @@ def load() -> ctypes.CDLL:
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    if L.tfg_abi_version() != ABI_VERSION:
+    # a same-box A/B may load an older library through TFG_LIB (one ABI back)
+    older_ok = "TFG_LIB" in os.environ and L.tfg_abi_version() == ABI_VERSION - 1
+    if L.tfg_abi_version() != ABI_VERSION and not older_ok:
         raise ImportError(f"{LIB_PATH}: ABI version {L.tfg_abi_version()} != {ABI_VERSION} (rebuild the library)")
     _lib = L
     return L
@@ -292,5 +297,6 @@ def exported_symbols() -> list[str]:
         "tfg_step", "tfg_set_fuse", "tfg_get_diag", "tfg_reset_diag", "tfg_sync",
         "tfg_fill_synthetic", "tfg_last_error", "tfg_terrain_from_dem", "tfg_ice_flow_edges", "tfg_ice_flow_dmax", "tfg_ice_flow_step", "tfg_ice_flow_run", "tfg_set_inputs", "tfg_get_outputs",
         "tfg_update", "tfg_update_many", "tfg_conduction_edges", "tfg_conduction_update", "tfg_conduction_off",
-        "tfg_nan_safe_launches", "tfg_set_step_form", "tfg_set_flux", "tfg_selftest_powers",
+        "tfg_nan_safe_launches", "tfg_set_step_form", "tfg_set_flux", "tfg_set_split", "tfg_join", "tfg_get_split",
+        "tfg_selftest_powers",
     ) if hasattr(L, n)]

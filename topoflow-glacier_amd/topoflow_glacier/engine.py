@@ -23,6 +23,7 @@ __all__ = ["GlacierEngine", "UpdateBatch", "params_from_config", "update_many"]
 
 _ENGINES = {"float32": nat.F32, "float64": nat.F64}
 _NP = {nat.F32: np.float32, nat.F64: np.float64}
+_SPLIT = {"auto": 0, "off": 1, "on": 2}  # include/tfg.h TFG_SPLIT_*
 
 
 def params_from_config(cfg) -> nat.TfgParams:
@@ -46,7 +47,7 @@ class GlacierEngine:
 
     def __init__(self, cfg, ny: int, nx: int, engine: str = "float32", device: int | None = None,
                  n_frames: int = 1, hist_depth: int = 1, n_catch: int = 1, fuse_steps: int | None = None,
-                 row0: int = 0, flux: str | None = None):
+                 row0: int = 0, flux: str | None = None, split: str = "auto"):
         self.lib = nat.load()
         self.cfg = cfg
         self.ny, self.nx, self.n = int(ny), int(nx), int(ny) * int(nx)
@@ -71,6 +72,11 @@ class GlacierEngine:
         if self.flux not in ("fp32", "fp64"):
             raise ValueError(f"flux must be 'fp32' or 'fp64', not {self.flux!r}")
         nat.check(self.lib.tfg_set_flux(self.h, 1 if self.flux == "fp64" else 0), self.h)
+        # two-part launches of a small fp32 grid on two streams (tfg_set_split): "auto", "off" or "on"
+        if split not in _SPLIT:
+            raise ValueError(f"split must be one of {sorted(_SPLIT)}, not {split!r}")
+        if hasattr(self.lib, "tfg_set_split"):
+            nat.check(self.lib.tfg_set_split(self.h, _SPLIT[split]), self.h)
         self.clock = StepClock(cfg.start_time, cfg.dt, cfg.lat, cfg.lon, getattr(cfg, "time_zone", None),
                                ring_len=self.ring_len)
         self.step_index = 0  # model steps completed
@@ -307,6 +313,21 @@ class GlacierEngine:
 
     def sync(self) -> None:
         self._chk(self.lib.tfg_sync(self.h))
+
+    def join(self) -> None:
+        """Order the engine's stream after the second part of split launches
+        (tfg_join; no host wait): before work the caller queues on that stream
+        itself, e.g. an event that marks the end of the steps."""
+        if hasattr(self.lib, "tfg_join"):
+            self._chk(self.lib.tfg_join(self.h))
+
+    def is_split(self) -> bool:
+        """Whether the next run() steps the grid as two parts on two streams (tfg_get_split)."""
+        if not hasattr(self.lib, "tfg_get_split"):
+            return False
+        v = ctypes.c_int()
+        self._chk(self.lib.tfg_get_split(self.h, ctypes.byref(v)))
+        return bool(v.value)
 
     def nan_safe_launches(self) -> int:
         """Launches that ran the fp32 engine's NaN-safe step form (include/tfg.h,
