@@ -41,6 +41,7 @@ sample (tests/harness.py flip_rule).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -974,6 +975,11 @@ def main(args=None):
     # the engine's stream would bracket the first parts only, so its launch time
     # is the span of the timed region (both parts joined) over the launches.
     split = eng.is_split()
+    # no collector pass inside the timed region: one took 8-11 ms of host time at a
+    # random tfg_step call (tests/diagnostics/split_first_launch.py), while the host
+    # runs at most two calls ahead of the device -- a tenth of config 2's 80 ms region
+    gc.collect()
+    gc.disable()
     barrier()
     t0 = time.perf_counter()
     for i in range(n_launch):
@@ -989,6 +995,7 @@ def main(args=None):
         ev[-1][1].record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     note(f"timed region: {n_launch} launches of {args.fuse} steps in {elapsed:.3f} s")
     if split:
         launch_ms = np.full(n_launch, ev[0][0].elapsed_time(ev[-1][1]) / n_launch)
