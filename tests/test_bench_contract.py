@@ -186,6 +186,8 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     assert mi["instances"] == 64 and mi["us_per_instance_step"] > 0 and mi["all_instances_equal"]
     ts = rf["traffic_source"]  # no PMC profile of this shape: traffic is null and says why
     assert rf["traffic"] is None and ts["reason"]
+    # 2^18 cells: split launches (tfg_set_split AUTO), timed as the span of the timed region
+    assert d["config"]["launch_parts"] == 2 and "span of the timed region" in rf["launch_time_source"]
 
 
 @pytest.mark.gpu

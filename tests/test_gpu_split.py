@@ -23,7 +23,7 @@ HIST = ("h_snow", "SM", "h_ice", "IM", "M_total", "RH")
 STATE = ("h_swe", "h_iwe", "Eccs", "Ecci", "n", "albedo")
 
 
-def _run(split, ny, nx, nsteps, fuse, flux="fp32", n_catch=1, nan_safe=False, reads=True):
+def _run(split, ny, nx, nsteps, fuse, flux="fp32", n_catch=1, nan_safe=False, reads=True, conduction=False):
     from topoflow_glacier.synthetic import diurnal_table
 
     e = make_engine(BASE_CFG, ny, nx, "float32", n_frames=24, hist_depth=nsteps, n_catch=n_catch,
@@ -34,6 +34,9 @@ def _run(split, ny, nx, nsteps, fuse, flux="fp32", n_catch=1, nan_safe=False, re
             e.set_field("catch_id", (np.arange(ny * nx) * 7 // (ny * nx) % n_catch).astype(np.int32))
         if nan_safe:
             e.set_step_form(True)
+        if conduction:  # the QC instance of k_fused, its Qc plane offset like the others
+            e.run(3)
+            e.conduction_update(0.3, 2.1, 30.0, 30.0, q_ground=0.5)
         was_split = e.is_split()
         mid = None
         k = 0
@@ -55,15 +58,16 @@ def _same(a, b):
     return np.array_equal(a, b, equal_nan=True)
 
 
-@pytest.mark.parametrize("ny,nx,nsteps,fuse,flux,n_catch,nan_safe", [
-    (37, 100, 60, 24, "fp32", 1, False),     # 3700 cells: 15 chunks, a part of 7
-    (64, 513, 50, 16, "fp32", 5, False),     # catchment bins in both parts
-    (37, 100, 30, 24, "fp64", 1, False),     # the fp64-flux form
-    (37, 100, 30, 24, "fp32", 1, True),      # the NaN-safe form
+@pytest.mark.parametrize("ny,nx,nsteps,fuse,flux,n_catch,nan_safe,conduction", [
+    (37, 100, 60, 24, "fp32", 1, False, False),     # 3700 cells: 15 chunks, a part of 7
+    (64, 513, 50, 16, "fp32", 5, False, False),     # catchment bins in both parts
+    (37, 100, 30, 24, "fp64", 1, False, False),     # the fp64-flux form
+    (37, 100, 30, 24, "fp32", 1, True, False),      # the NaN-safe form
+    (37, 100, 30, 24, "fp32", 1, False, True),      # the lateral conduction term on
 ])
-def test_split_equals_one_launch_bit_for_bit(ny, nx, nsteps, fuse, flux, n_catch, nan_safe):
-    s1, h1, st1, d1, m1 = _run("on", ny, nx, nsteps, fuse, flux, n_catch, nan_safe)
-    s0, h0, st0, d0, m0 = _run("off", ny, nx, nsteps, fuse, flux, n_catch, nan_safe)
+def test_split_equals_one_launch_bit_for_bit(ny, nx, nsteps, fuse, flux, n_catch, nan_safe, conduction):
+    s1, h1, st1, d1, m1 = _run("on", ny, nx, nsteps, fuse, flux, n_catch, nan_safe, conduction=conduction)
+    s0, h0, st0, d0, m0 = _run("off", ny, nx, nsteps, fuse, flux, n_catch, nan_safe, conduction=conduction)
     assert s1 and not s0
     for v in HIST:
         assert _same(h1[v], h0[v]), v
