@@ -355,8 +355,12 @@ def split_engine(engine: str) -> tuple[str, str]:
 
 
 def make_engine(cfg: dict, ny: int, nx: int, engine: str, n_frames: int, hist_depth: int, n_catch: int = 1,
-                fuse_steps: int = 24, row0: int = 0, flux: str = "fp32", split: str = "auto"):
+                fuse_steps: int = 24, row0: int = 0, flux: str = "fp32", split: str | None = None):
+    """split: tfg_set_split's mode; by default "auto", or TFG_TEST_SPLIT ("on": every
+    fp32 grid of the suite stepped as two parts on two streams, a stress run)."""
     from topoflow_glacier.engine import GlacierEngine
+
+    split = split or os.environ.get("TFG_TEST_SPLIT", "auto")
 
     engine, f = split_engine(engine)
     return GlacierEngine(cfg_object(cfg), ny, nx, engine=engine, device=0, n_frames=n_frames,
