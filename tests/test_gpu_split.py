@@ -88,7 +88,7 @@ def test_auto_splits_a_config2_sized_grid_and_matches():
     for v in STATE:
         assert _same(st1[v], st0[v]), v
     assert _same(d1, d0)
-    e = make_engine(BASE_CFG, 64, 128, "float32", n_frames=1, hist_depth=1)
+    e = make_engine(BASE_CFG, 64, 128, "float32", n_frames=1, hist_depth=1, split="auto")
     try:
         assert not e.is_split()
     finally:
