@@ -24,6 +24,23 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 MARGIN_TOL = 8e-6
+_FIELDS = ("global_rows", "max_floored_rel", "max_floored_rel_at", "max_floored_rel_fp64_baseline", "melt_out_flips",
+           "flips_fp64_baseline", "depletion_steps", "depletion_steps_fp64_baseline", "melt_onsets_explained")
+
+
+def _record(name, par):
+    """Print the sample's parity record and, when $TFG_REPORT_DIR is set, write
+    it there as deep_<name>.json (profiles/r6d_deep_samples.json collects them)."""
+    import json
+    import os
+
+    rec = {k: par.get(k) for k in _FIELDS}
+    print(rec)
+    d = os.environ.get("TFG_REPORT_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"deep_{name}.json"), "w") as f:
+            json.dump(rec, f, indent=1, default=str)
 
 
 def test_n4_rank0_deep_launch_sample(monkeypatch):
@@ -51,9 +68,7 @@ def test_n4_rank0_deep_launch_sample(monkeypatch):
         eng.close()
     assert cap["plan"]["launch_steps"] == [1, 384] and cap["plan"]["rows"] == 10
     par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
-    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
-                               "flips_fp64_baseline", "depletion_steps", "depletion_steps_fp64_baseline",
-                               "melt_onsets_explained")})
+    _record("n4_rank0_fp32", par)
     assert par["global_rows"] == [0, 9]
     assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
     assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
@@ -107,9 +122,7 @@ def _timed_depth_sample(monkeypatch, argv, world, rank, want_fuse, want_rows, fl
         eng.close()
     assert cap["plan"]["launch_steps"] == [1, want_fuse]
     par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
-    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
-                               "flips_fp64_baseline", "depletion_steps", "depletion_steps_fp64_baseline",
-                               "melt_onsets_explained")})
+    _record(f"{args.ny}x{args.nx}_n{world}_rank{rank}_{flux}", par)
     assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
     assert par["max_floored_rel"] <= MARGIN_TOL, par["max_floored_rel_at"]
     _exclusions_do_not_grow(par, flux)
@@ -172,9 +185,7 @@ def test_n4_rank2_deep_launch_sample(monkeypatch):
         eng.close()
     assert cap["plan"]["launch_steps"] == [1, 384]
     par, _ = bench.sample_parity(args, plan, world, rank, bench._cpu_threads(), cap)
-    print({k: par[k] for k in ("global_rows", "max_floored_rel", "max_floored_rel_fp64_baseline", "melt_out_flips",
-                               "flips_fp64_baseline", "depletion_steps", "depletion_steps_fp64_baseline",
-                               "melt_onsets_explained")})
+    _record("n4_rank2_fp32", par)
     assert par["global_rows"] == [4096, 4103]
     assert par["ok"], {k: par[k] for k in ("max_floored_rel", "genuine_mismatches", "flip_rule", "mass_balance")}
     assert par["max_floored_rel"] <= 1e-5, par["max_floored_rel_at"]
